@@ -1,0 +1,294 @@
+// ff.hpp — BLS12-381 Fr (255-bit) and Fp (381-bit) Montgomery arithmetic for gfx950.
+//
+// Restates the field arithmetic of the un-vendored `bls-12-381` crate:
+// Fr is 4x64 Montgomery with R = 2^256 (pinned by /root/reference/src/lib.rs:583-588),
+// Fp is 6x64 Montgomery with R = 2^384. In registers we use 32-bit limbs (8 for Fr, 12
+// for Fp): CDNA4 has no 64x64 multiplier, and the 32x32->64 `v_mad_u64_u32` is the
+// natural building block. The memory image is identical to 4/6 little-endian u64 limbs,
+// so the ABI layout (include/plk.h) is loaded without any conversion.
+//
+// Multiplication is CIOS with the "spare bit" shortcut: both moduli have their top
+// 32-bit word below 2^31 - 1, so the running value never needs an (N+1)-th word and
+// the result lands in [0, 2p) before one conditional subtraction. Every function
+// returns canonical (fully reduced) values.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define PLK_HD __host__ __device__ __forceinline__
+#else
+#define PLK_HD inline
+#endif
+
+namespace plk {
+
+struct FrCfg {
+  static constexpr int N = 8;
+  // r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+  static constexpr uint32_t P[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                    0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+  static constexpr uint32_t INV = 0xffffffffu;  // -r^-1 mod 2^32
+  static constexpr uint64_t INV64 = 0xfffffffeffffffffull;  // -r^-1 mod 2^64
+  // R mod r  (Montgomery one)
+  static constexpr uint32_t ONE[8] = {0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau,
+                                      0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u};
+  // R^2 mod r
+  static constexpr uint32_t R2[8] = {0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu,
+                                     0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u};
+};
+
+struct FpCfg {
+  static constexpr int N = 12;
+  static constexpr uint32_t P[12] = {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu,
+                                     0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, 0x64774b84u,
+                                     0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
+  static constexpr uint32_t INV = 0xfffcfffdu;  // -p^-1 mod 2^32
+  static constexpr uint64_t INV64 = 0x89f3fffcfffcfffdull;  // -p^-1 mod 2^64
+  static constexpr uint32_t ONE[12] = {0x0002fffdu, 0x76090000u, 0xc40c0002u, 0xebf4000bu,
+                                       0x53c758bau, 0x5f489857u, 0x70525745u, 0x77ce5853u,
+                                       0xa256ec6du, 0x5c071a97u, 0xfa80e493u, 0x15f65ec3u};
+  static constexpr uint32_t R2[12] = {0x1c341746u, 0xf4df1f34u, 0x09d104f1u, 0x0a76e6a6u,
+                                      0x4c95b6d5u, 0x8de5476cu, 0x939d83c0u, 0x67eb88a9u,
+                                      0xb519952du, 0x9a793e85u, 0x92cae3aau, 0x11988fe5u};
+};
+
+template <class C>
+struct alignas(16) Fe {
+  uint32_t v[C::N];
+};
+
+using Fr = Fe<FrCfg>;
+using Fp = Fe<FpCfg>;
+
+// ----------------------------------------------------------------------------- basics
+template <class C>
+PLK_HD Fe<C> fe_zero() {
+  Fe<C> r;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) r.v[i] = 0;
+  return r;
+}
+
+template <class C>
+PLK_HD Fe<C> fe_one() {
+  Fe<C> r;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) r.v[i] = C::ONE[i];
+  return r;
+}
+
+template <class C>
+PLK_HD bool fe_is_zero(const Fe<C>& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) acc |= a.v[i];
+  return acc == 0;
+}
+
+template <class C>
+PLK_HD bool fe_eq(const Fe<C>& a, const Fe<C>& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+// r = a - p if a >= p else a (a < 2p)
+template <class C>
+PLK_HD void fe_reduce_once(Fe<C>& a) {
+  uint32_t d[C::N];
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) {
+    uint64_t t = (uint64_t)a.v[i] - C::P[i] - borrow;
+    d[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  // borrow == 1  <=>  a < p  -> keep a
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) a.v[i] = borrow ? a.v[i] : d[i];
+}
+
+template <class C>
+PLK_HD Fe<C> fe_add(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> r;
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) {
+    uint64_t t = (uint64_t)a.v[i] + b.v[i] + carry;
+    r.v[i] = (uint32_t)t;
+    carry = (uint32_t)(t >> 32);
+  }
+  // both moduli leave a spare top bit, so a + b < 2p < 2^(32N): no carry out
+  fe_reduce_once(r);
+  return r;
+}
+
+template <class C>
+PLK_HD Fe<C> fe_sub(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> r;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) {
+    uint64_t t = (uint64_t)a.v[i] - b.v[i] - borrow;
+    r.v[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  // if it went negative, add p back
+  uint32_t mask = 0u - borrow;
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) {
+    uint64_t t = (uint64_t)r.v[i] + (C::P[i] & mask) + carry;
+    r.v[i] = (uint32_t)t;
+    carry = (uint32_t)(t >> 32);
+  }
+  return r;
+}
+
+template <class C>
+PLK_HD Fe<C> fe_neg(const Fe<C>& a) {
+  return fe_sub(fe_zero<C>(), a);
+}
+
+template <class C>
+PLK_HD Fe<C> fe_dbl(const Fe<C>& a) {
+  return fe_add(a, a);
+}
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host path: the same Montgomery product on 64-bit limbs (identical memory image). The
+// host only runs the MSM's short serial tail and table set-up, where latency matters.
+template <class C>
+inline Fe<C> fe_mul_host64(const Fe<C>& a, const Fe<C>& b) {
+  constexpr int M = C::N / 2;
+  uint64_t A[M], B[M], P[M], t[M];
+  for (int i = 0; i < M; ++i) {
+    A[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
+    B[i] = (uint64_t)b.v[2 * i] | ((uint64_t)b.v[2 * i + 1] << 32);
+    P[i] = (uint64_t)C::P[2 * i] | ((uint64_t)C::P[2 * i + 1] << 32);
+    t[i] = 0;
+  }
+  for (int i = 0; i < M; ++i) {
+    unsigned __int128 c = 0;
+    for (int j = 0; j < M; ++j) {
+      c += (unsigned __int128)A[j] * B[i] + t[j];
+      t[j] = (uint64_t)c;
+      c >>= 64;
+    }
+    const uint64_t tn = (uint64_t)c;
+    const uint64_t m = t[0] * C::INV64;
+    c = (unsigned __int128)m * P[0] + t[0];
+    c >>= 64;
+    for (int j = 1; j < M; ++j) {
+      c += (unsigned __int128)m * P[j] + t[j];
+      t[j - 1] = (uint64_t)c;
+      c >>= 64;
+    }
+    t[M - 1] = tn + (uint64_t)c;
+  }
+  Fe<C> r;
+  for (int i = 0; i < M; ++i) {
+    r.v[2 * i] = (uint32_t)t[i];
+    r.v[2 * i + 1] = (uint32_t)(t[i] >> 32);
+  }
+  fe_reduce_once(r);
+  return r;
+}
+#endif
+
+// Montgomery product a*b*R^-1 mod p (CIOS, spare-bit form).
+template <class C>
+PLK_HD Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return fe_mul_host64(a, b);
+#else
+  constexpr int N = C::N;
+  uint32_t t[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t bi = b.v[i];
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      uint64_t s = (uint64_t)a.v[j] * bi + t[j] + c;
+      t[j] = (uint32_t)s;
+      c = s >> 32;
+    }
+    const uint32_t tn = (uint32_t)c;
+    const uint32_t m = t[0] * C::INV;
+    uint64_t s = (uint64_t)m * C::P[0] + t[0];
+    c = s >> 32;
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+      s = (uint64_t)m * C::P[j] + t[j] + c;
+      t[j - 1] = (uint32_t)s;
+      c = s >> 32;
+    }
+    t[N - 1] = tn + (uint32_t)c;
+  }
+  Fe<C> r;
+#pragma unroll
+  for (int j = 0; j < N; ++j) r.v[j] = t[j];
+  fe_reduce_once(r);
+  return r;
+#endif
+}
+
+template <class C>
+PLK_HD Fe<C> fe_sqr(const Fe<C>& a) {
+  return fe_mul(a, a);
+}
+
+template <class C>
+PLK_HD Fe<C> fe_to_mont(const Fe<C>& a) {
+  Fe<C> r2;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) r2.v[i] = C::R2[i];
+  return fe_mul(a, r2);
+}
+
+template <class C>
+PLK_HD Fe<C> fe_from_mont(const Fe<C>& a) {
+  Fe<C> one = fe_zero<C>();
+  one.v[0] = 1;
+  return fe_mul(a, one);
+}
+
+// a^e for a little-endian exponent of `words` 32-bit words (square-and-multiply, MSB first)
+template <class C>
+PLK_HD Fe<C> fe_pow(const Fe<C>& a, const uint32_t* e, int words) {
+  Fe<C> r = fe_one<C>();
+  for (int w = words - 1; w >= 0; --w) {
+    for (int b = 31; b >= 0; --b) {
+      r = fe_sqr(r);
+      if ((e[w] >> b) & 1u) r = fe_mul(r, a);
+    }
+  }
+  return r;
+}
+
+template <class C>
+PLK_HD Fe<C> fe_pow_u64(const Fe<C>& a, uint64_t e) {
+  uint32_t w[2] = {(uint32_t)e, (uint32_t)(e >> 32)};
+  return fe_pow(a, w, 2);
+}
+
+// Fermat inversion a^(p-2); inverse of zero is zero.
+template <class C>
+PLK_HD Fe<C> fe_inv(const Fe<C>& a) {
+  uint32_t e[C::N];
+  uint32_t borrow = 2;
+#pragma unroll
+  for (int i = 0; i < C::N; ++i) {
+    uint64_t t = (uint64_t)C::P[i] - borrow;
+    e[i] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+  return fe_pow(a, e, C::N);
+}
+
+}  // namespace plk

@@ -1,0 +1,132 @@
+// internal.hpp — shared runtime objects behind the C ABI (include/plk.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/plk.h"
+#include "ff.hpp"
+#include "g1.hpp"
+
+namespace plk {
+
+#define PLK_HIP_TRY(expr)                                        \
+  do {                                                           \
+    hipError_t _e = (expr);                                      \
+    if (_e != hipSuccess) {                                      \
+      last_hip_error() = _e;                                     \
+      return (_e == hipErrorOutOfMemory) ? PLK_E_OOM : PLK_E_DEVICE; \
+    }                                                            \
+  } while (0)
+
+hipError_t& last_hip_error();
+
+// Device buffer owned by a context object.
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (ptr) (void)hipFree(ptr);
+  }
+  int alloc(size_t b) {
+    if (ptr && bytes >= b) return PLK_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    if (b == 0) return PLK_OK;
+    hipError_t e = hipMalloc(&ptr, b);
+    if (e != hipSuccess) {
+      ptr = nullptr;
+      last_hip_error() = e;
+      return e == hipErrorOutOfMemory ? PLK_E_OOM : PLK_E_DEVICE;
+    }
+    bytes = b;
+    return PLK_OK;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(ptr);
+  }
+};
+
+struct NttPass {
+  uint32_t lp, lr, lt;  // log2 of: sub-transform length so far, radix, columns per block
+};
+
+}  // namespace plk
+
+struct plk_domain {
+  plk_ctx* ctx = nullptr;
+  uint32_t log_n = 0;
+  uint64_t n = 0;
+  plk::Fr omega, omega_inv, n_inv, g, g_inv;  // Montgomery form (host copies)
+  plk::DevBuf tw_fwd;        // w^e, e < n
+  plk::DevBuf tw_inv;        // w^-e, e < n
+  plk::DevBuf coset_pow;     // g^e, e < n
+  plk::DevBuf icoset_scale;  // n^-1 * g^-e, e < n
+  plk::DevBuf scratch;       // 2n elements (default scratch for plk_ntt_dev)
+  plk::DevBuf io;            // n elements (host-buffer entry points stage through it)
+  std::vector<plk::NttPass> plan;
+  uint32_t le = 10;          // log2 elements per workgroup
+};
+
+namespace plk {
+struct MsmWorkspace;
+}
+
+struct plk_srs {
+  plk_ctx* ctx = nullptr;
+  size_t n = 0;              // number of SRS points
+  uint32_t c = 16;           // window bits
+  uint32_t windows = 16;     // ceil(256 / c)
+  plk::DevBuf points;        // affine, plk::G1Affine (96 B), n entries; inf flags separate
+  plk::DevBuf inf;           // uint8 per point
+  plk::DevBuf table;         // precomputed 2^(c*w) * P_i, affine, windows * n entries
+  plk::DevBuf table_inf;     // uint8, windows * n
+  bool has_inf = false;      // any point at infinity in the SRS (slow-path flag checks)
+  plk::DevBuf staging;       // host-scalar entry points stage through it
+  std::unique_ptr<plk::MsmWorkspace> ws;
+  float last_accumulate_ms = 0.f;
+  uint64_t last_point_adds = 0;
+  plk_srs();
+  ~plk_srs();
+};
+
+struct plk_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::map<uint32_t, std::unique_ptr<plk_domain>> domains;
+  std::mutex mu;
+};
+
+namespace plk {
+// RAII device guard
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int ntt_build_domain(plk_domain* d);
+int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset,
+            Fr* scratch, hipStream_t stream, uint32_t count);
+int msm_prepare_srs(plk_srs* s, hipStream_t stream);
+int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g1* out,
+            hipStream_t stream);
+void fr_root_of_unity(uint32_t log_n, Fr& omega);
+int ntt_vanishing(plk_domain* d, uint64_t deg, Fr* d_out, hipStream_t s);
+int srs_generate(plk_srs* s, const Fr& tau_mont, hipStream_t stream);
+}  // namespace plk

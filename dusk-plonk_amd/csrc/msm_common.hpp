@@ -1,0 +1,73 @@
+// msm_common.hpp — device load/store helpers and the per-SRS MSM workspace.
+#pragma once
+#include "internal.hpp"
+
+namespace plk {
+
+constexpr uint32_t kChunk = 64;     // points per accumulation task
+constexpr uint32_t kBatchAff = 32;  // points per batch-inversion chunk
+
+struct MsmCfg {
+  uint32_t c, W, B;
+};
+
+__device__ __forceinline__ void ld_fp(const uint32_t* p, Fp& r) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    uint4 a = q[i];
+    r.v[4 * i] = a.x; r.v[4 * i + 1] = a.y; r.v[4 * i + 2] = a.z; r.v[4 * i + 3] = a.w;
+  }
+}
+
+__device__ __forceinline__ void st_fp(uint32_t* p, const Fp& v) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) q[i] = make_uint4(v.v[4 * i], v.v[4 * i + 1], v.v[4 * i + 2], v.v[4 * i + 3]);
+}
+
+__device__ __forceinline__ void ld_aff(const G1Affine* p, Fp& x, Fp& y) {
+  ld_fp(reinterpret_cast<const uint32_t*>(p), x);
+  ld_fp(reinterpret_cast<const uint32_t*>(p) + 12, y);
+}
+
+__device__ __forceinline__ void st_aff(G1Affine* p, const Fp& x, const Fp& y) {
+  st_fp(reinterpret_cast<uint32_t*>(p), x);
+  st_fp(reinterpret_cast<uint32_t*>(p) + 12, y);
+}
+
+__device__ __forceinline__ void ld_xyzz(const G1xyzz* p, G1xyzz& r) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+  ld_fp(q, r.X); ld_fp(q + 12, r.Y); ld_fp(q + 24, r.ZZ); ld_fp(q + 36, r.ZZZ);
+}
+
+__device__ __forceinline__ void st_xyzz(G1xyzz* p, const G1xyzz& r) {
+  uint32_t* q = reinterpret_cast<uint32_t*>(p);
+  st_fp(q, r.X); st_fp(q + 12, r.Y); st_fp(q + 24, r.ZZ); st_fp(q + 36, r.ZZZ);
+}
+
+__device__ __forceinline__ Fr ld_fr(const Fr* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  Fr r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+
+
+inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+struct MsmWorkspace {
+  DevBuf counts, offsets, task_off, cursor, sorted, tasks, partials, buckets, bits1, bits2, flag;
+  size_t cap_len = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  ~MsmWorkspace() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+  }
+};
+
+int ws_reserve(plk_srs* s, size_t len);
+
+}  // namespace plk

@@ -1,0 +1,281 @@
+// ntt.hip — BLS12-381 Fr NTT family on gfx950: Fft::{dft, idft, coset_dft, coset_idft}.
+//
+// Reference semantics (poly_commit::Fft, un-vendored): natural order
+// in and out, w = ROOT_OF_UNITY^(2^(32-k)), elements[i] = w^i (permutation.rs:148),
+// idft scaled by n^-1, cosets over g*H with g = 7 (quotient_poly.rs:54-58,115).
+//
+// Algorithm: self-sorting (Stockham) decomposition into P passes of radix R = 2^lr.
+// A pass reads the R inputs x[i + j*N/R] (j < R) of T consecutive i (coalesced T-wide
+// column groups), applies the inter-pass twiddle w_{Rp}^{jk} (k = i mod p), runs the
+// R-point sub-DFT in LDS (radix-2 DIF stages, twiddles staged in LDS), and writes
+// Y[k + m p] of each length-Rp sub-transform to (i-k)*R + k + m*p. No bit-reversal pass
+// is needed: the last pass leaves natural order. The coset pre-scale g^e is fused into
+// the first pass' loads, zero padding (len_in < n) into the same loads, and the n^-1
+// (or n^-1 g^-e) post-scale into the last pass' stores.
+//
+// HBM traffic per transform: P * 2 * N * 32 B (P = 3 at N = 2^20..2^24).
+#include "internal.hpp"
+
+namespace plk {
+
+namespace {
+
+constexpr uint32_t kMaxLr = 8;   // radix up to 256
+constexpr uint32_t kMaxLe = 10;  // 1024 elements (32 KiB) per workgroup
+
+__device__ __forceinline__ Fr ld_fr(const Fr* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  Fr r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+
+__device__ __forceinline__ void st_fr(Fr* p, const Fr& v) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+
+__device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
+  return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0u;
+}
+
+// One Stockham pass. PRE: 0 none, 1 multiply input e by pre[e] (coset g^e).
+// POST: 0 none, 1 multiply by post_scalar, 2 multiply output e by post[e].
+template <int PRE, int POST>
+__global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
+                                                  const Fr* __restrict__ tw,
+                                                  const Fr* __restrict__ pre,
+                                                  const Fr* __restrict__ post, Fr post_scalar,
+                                                  uint32_t log_n, uint32_t lp, uint32_t lr,
+                                                  uint32_t lt, uint64_t len_in, uint64_t n_stride) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Fr* data = reinterpret_cast<Fr*>(smem);
+  const uint32_t R = 1u << lr, T = 1u << lt, p = 1u << lp;
+  const uint32_t E = R << lt;
+  Fr* twl = data + E;  // R/2 inner twiddles w_R^x
+
+  const size_t voff = (size_t)blockIdx.y * n_stride;
+  in += voff;
+  out += voff;
+
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  const uint32_t nr_log = log_n - lr;  // log2(N/R)
+  const uint32_t i0 = blockIdx.x << lt;
+
+  for (uint32_t x = tid; x < (R >> 1); x += bd) st_fr(&twl[x], ld_fr(&tw[(size_t)x << nr_log]));
+
+  const uint32_t tw_shift = log_n - lr - lp;  // w_{Rp}^{jk} = w_N^{jk * N/(Rp)}
+  for (uint32_t e = tid; e < E; e += bd) {
+    const uint32_t t = e & (T - 1), j = e >> lt;
+    const uint32_t i = i0 + t;
+    const size_t g = (size_t)i + ((size_t)j << nr_log);
+    Fr v;
+    if (g < len_in) {
+      v = ld_fr(&in[g]);
+      if (PRE == 1) v = fe_mul(v, ld_fr(&pre[g]));
+    } else {
+      v = fe_zero<FrCfg>();
+    }
+    const uint32_t k = i & (p - 1);
+    if (j != 0 && k != 0) v = fe_mul(v, ld_fr(&tw[(size_t)(j * k) << tw_shift]));
+    st_fr(&data[(j << lt) + t], v);
+  }
+  __syncthreads();
+
+  // R-point DIF (natural in, bit-reversed out) on each of the T columns
+  for (int lh = (int)lr - 1; lh >= 0; --lh) {
+    const uint32_t h = 1u << lh;
+    for (uint32_t b = tid; b < (E >> 1); b += bd) {
+      const uint32_t t = b & (T - 1), jb = b >> lt;
+      const uint32_t r = jb & (h - 1);
+      const uint32_t j1 = ((jb >> lh) << (lh + 1)) + r, j2 = j1 + h;
+      const Fr a = ld_fr(&data[(j1 << lt) + t]);
+      const Fr c = ld_fr(&data[(j2 << lt) + t]);
+      st_fr(&data[(j1 << lt) + t], fe_add(a, c));
+      Fr d = fe_sub(a, c);
+      if (r != 0) d = fe_mul(d, ld_fr(&twl[r << (lr - 1 - lh)]));
+      st_fr(&data[(j2 << lt) + t], d);
+    }
+    __syncthreads();
+  }
+
+  for (uint32_t o = tid; o < E; o += bd) {
+    uint32_t t, m;
+    if (p >= T) {
+      t = o & (T - 1);
+      m = o >> lt;
+    } else {  // o = u*pR + m*p + s, t = u*p + s: contiguous output run per workgroup
+      const uint32_t s = o & (p - 1);
+      m = (o >> lp) & (R - 1);
+      t = ((o >> (lp + lr)) << lp) + s;
+    }
+    const uint32_t i = i0 + t;
+    const uint32_t k = i & (p - 1);
+    const size_t pos = ((size_t)(i - k) << lr) + k + ((size_t)m << lp);
+    Fr v = ld_fr(&data[(bitrev(m, lr) << lt) + t]);
+    if (POST == 1) v = fe_mul(v, post_scalar);
+    if (POST == 2) v = fe_mul(v, ld_fr(&post[pos]));
+    st_fr(&out[pos], v);
+  }
+}
+
+// table[e] = base^e * scale for e < n (exact powers; one pow per element)
+__global__ void k_power_table(Fr* __restrict__ out, Fr base, Fr scale, uint64_t n) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  st_fr(&out[e], fe_mul(fe_pow_u64(base, e), scale));
+}
+
+__global__ void k_copy_pad(const Fr* __restrict__ in, Fr* __restrict__ out, uint64_t len_in,
+                           uint64_t n) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  st_fr(&out[e], e < len_in ? ld_fr(&in[e]) : fe_zero<FrCfg>());
+}
+
+// v_h[i] = (g w^i)^deg - 1 = g^deg * (w^deg)^i - 1
+__global__ void k_vanishing(Fr* __restrict__ out, Fr gdeg, Fr wdeg, uint64_t n) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  st_fr(&out[e], fe_sub(fe_mul(gdeg, fe_pow_u64(wdeg, e)), fe_one<FrCfg>()));
+}
+
+}  // namespace
+
+// ROOT_OF_UNITY = 7^((r-1)/2^32) (Montgomery form), squared down to order 2^log_n
+void fr_root_of_unity(uint32_t log_n, Fr& omega) {
+  // canonical 0x16a2a19edfe81f20d09b681922c813b4b63683508c2280b93829971f439f0d2b
+  static const uint32_t root[8] = {0x439f0d2bu, 0x3829971fu, 0x8c2280b9u, 0xb6368350u,
+                                   0x22c813b4u, 0xd09b6819u, 0xdfe81f20u, 0x16a2a19eu};
+  Fr w;
+  for (int i = 0; i < 8; ++i) w.v[i] = root[i];
+  w = fe_to_mont(w);
+  for (uint32_t s = log_n; s < 32; ++s) w = fe_sqr(w);
+  omega = w;
+}
+
+static void plan_domain(plk_domain* d) {
+  const uint32_t L = d->log_n;
+  d->plan.clear();
+  if (L == 0) return;
+  // elements per workgroup: keep >= ~256 workgroups when the transform allows it
+  uint32_t le = L > 8 ? L - 8 : 1;
+  if (le < 6) le = L < 6 ? L : 6;
+  if (le > kMaxLe) le = kMaxLe;
+  const uint32_t max_lr = le < kMaxLr ? le : kMaxLr;
+  const uint32_t P = (L + max_lr - 1) / max_lr;
+  uint32_t lp = 0;
+  for (uint32_t q = 0; q < P; ++q) {
+    const uint32_t rem = L - lp, left = P - q;
+    const uint32_t lr = (rem + left - 1) / left;
+    uint32_t lt = le - lr;
+    if (lt > L - lr) lt = L - lr;
+    d->plan.push_back(NttPass{lp, lr, lt});
+    lp += lr;
+  }
+  d->le = le;
+}
+
+int ntt_build_domain(plk_domain* d) {
+  const uint64_t n = d->n;
+  fr_root_of_unity(d->log_n, d->omega);
+  d->omega_inv = fe_inv(d->omega);
+  Fr nf = fe_zero<FrCfg>();
+  nf.v[0] = (uint32_t)n;
+  nf.v[1] = (uint32_t)(n >> 32);
+  nf = fe_to_mont(nf);
+  d->n_inv = fe_inv(nf);
+  Fr g = fe_zero<FrCfg>();
+  g.v[0] = 7;
+  d->g = fe_to_mont(g);
+  d->g_inv = fe_inv(d->g);
+  plan_domain(d);
+
+  int st;
+  if ((st = d->tw_fwd.alloc(n * sizeof(Fr)))) return st;
+  if ((st = d->tw_inv.alloc(n * sizeof(Fr)))) return st;
+  if ((st = d->coset_pow.alloc(n * sizeof(Fr)))) return st;
+  if ((st = d->icoset_scale.alloc(n * sizeof(Fr)))) return st;
+  hipStream_t s = d->ctx->stream;
+  const uint32_t bs = 256;
+  const uint32_t nb = (uint32_t)((n + bs - 1) / bs);
+  const Fr one = fe_one<FrCfg>();
+  hipLaunchKernelGGL(k_power_table, dim3(nb), dim3(bs), 0, s, d->tw_fwd.as<Fr>(), d->omega, one, n);
+  hipLaunchKernelGGL(k_power_table, dim3(nb), dim3(bs), 0, s, d->tw_inv.as<Fr>(), d->omega_inv, one, n);
+  hipLaunchKernelGGL(k_power_table, dim3(nb), dim3(bs), 0, s, d->coset_pow.as<Fr>(), d->g, one, n);
+  hipLaunchKernelGGL(k_power_table, dim3(nb), dim3(bs), 0, s, d->icoset_scale.as<Fr>(), d->g_inv,
+                     d->n_inv, n);
+  PLK_HIP_TRY(hipGetLastError());
+  PLK_HIP_TRY(hipStreamSynchronize(s));
+  return PLK_OK;
+}
+
+int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset, Fr* scratch,
+            hipStream_t stream, uint32_t count) {
+  const uint64_t n = d->n;
+  if (len_in > n) return PLK_E_ARG;
+  if (n == 1) {  // size-1 transform: identity (times n^-1 = 1, g^0 = 1)
+    for (uint32_t v = 0; v < count; ++v) {
+      if (len_in == 0) {
+        PLK_HIP_TRY(hipMemsetAsync(out + v, 0, sizeof(Fr), stream));
+      } else if (in != out) {
+        PLK_HIP_TRY(hipMemcpyAsync(out + v, in + v, sizeof(Fr), hipMemcpyDeviceToDevice, stream));
+      }
+    }
+    return PLK_OK;
+  }
+  int st;
+  if (!scratch) {
+    if ((st = d->scratch.alloc(2 * n * sizeof(Fr) * (count > 1 ? count : 1)))) return st;
+    scratch = d->scratch.as<Fr>();
+  }
+  const size_t P = d->plan.size();
+  Fr* s1 = scratch;
+  Fr* s2 = scratch + n * count;
+  const Fr* tw = dir > 0 ? d->tw_fwd.as<Fr>() : d->tw_inv.as<Fr>();
+  const Fr* src = in;
+  for (size_t q = 0; q < P; ++q) {
+    const NttPass& ps = d->plan[q];
+    Fr* dst = (q + 1 == P) ? out : ((q & 1) ? s2 : s1);
+    const bool first = q == 0, last = q + 1 == P;
+    const uint32_t E = 1u << (ps.lr + ps.lt);
+    uint32_t bd = E / 4;
+    if (bd < 64) bd = 64;
+    if (bd > 256) bd = 256;
+    const uint32_t blocks = (uint32_t)(n >> (ps.lr + ps.lt));
+    const size_t lds = ((size_t)E + (1u << ps.lr) / 2) * sizeof(Fr);
+    const int pre = (first && dir > 0 && coset) ? 1 : 0;
+    const int post = (last && dir < 0) ? (coset ? 2 : 1) : 0;
+    const uint64_t lin = first ? len_in : n;
+    dim3 grid(blocks, count);
+#define PLK_LAUNCH(PRE, POST)                                                                 \
+  hipLaunchKernelGGL((k_ntt_pass<PRE, POST>), grid, dim3(bd), lds, stream, src, dst, tw,     \
+                     d->coset_pow.as<Fr>(), d->icoset_scale.as<Fr>(), d->n_inv, d->log_n,   \
+                     ps.lp, ps.lr, ps.lt, lin, (uint64_t)n)
+    if (pre == 0 && post == 0) PLK_LAUNCH(0, 0);
+    else if (pre == 1 && post == 0) PLK_LAUNCH(1, 0);
+    else if (pre == 0 && post == 1) PLK_LAUNCH(0, 1);
+    else if (pre == 0 && post == 2) PLK_LAUNCH(0, 2);
+    else if (pre == 1 && post == 1) PLK_LAUNCH(1, 1);
+    else PLK_LAUNCH(1, 2);
+#undef PLK_LAUNCH
+    PLK_HIP_TRY(hipGetLastError());
+    src = dst;
+  }
+  return PLK_OK;
+}
+
+int ntt_vanishing(plk_domain* d, uint64_t deg, Fr* d_out, hipStream_t s) {
+  const Fr gdeg = fe_pow_u64(d->g, deg);
+  const Fr wdeg = fe_pow_u64(d->omega, deg);
+  const uint32_t bs = 256;
+  const uint32_t nb = (uint32_t)((d->n + bs - 1) / bs);
+  hipLaunchKernelGGL(k_vanishing, dim3(nb), dim3(bs), 0, s, d_out, gdeg, wdeg, (uint64_t)d->n);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+}  // namespace plk

@@ -1,0 +1,149 @@
+// srs.hip — PlonkParams::setup (SRS generation) and the MSM window tables, on gfx950.
+//
+// setup(k, rng) (zksnarks, un-vendored; tests/*.rs:24) restated with an
+// explicit secret tau: g1[i] = [tau^i] G1. The MSM (msm.hip) additionally needs
+// table[w][i] = 2^(c*w) * g1[i] in affine form; both are produced here with XYZZ
+// arithmetic and converted to affine by batch inversion (Montgomery's trick, one Fermat
+// inversion per kBatchAff points).
+#include <hip/hip_runtime.h>
+
+#include "internal.hpp"
+#include "msm_common.hpp"
+
+namespace plk {
+
+namespace {
+
+// ---- table construction --------------------------------------------------------------
+// temp[i] = 2^c * src[i]  (XYZZ)
+__global__ void __launch_bounds__(256) k_double_c(const G1Affine* __restrict__ src, const uint8_t* __restrict__ src_inf,
+                           uint64_t n, uint32_t c, G1xyzz* __restrict__ temp) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1xyzz acc;
+  if (src_inf[i]) {
+    acc = xyzz_infinity();
+  } else {
+    Fp x, y;
+    ld_aff(&src[i], x, y);
+    acc = xyzz_from_affine(G1Affine{x, y});
+  }
+  for (uint32_t k = 0; k < c; ++k) acc = xyzz_dbl(acc);
+  st_xyzz(&temp[i], acc);
+}
+
+// temp[i] = [tau^i] G  (XYZZ), double-and-add on the canonical exponent
+__global__ void __launch_bounds__(128) k_srs_powers(Fr tau, G1Affine gen, uint64_t n, G1xyzz* __restrict__ temp) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr s = fe_from_mont(fe_pow_u64(tau, i));
+  G1xyzz acc = xyzz_infinity();
+  for (int b = 254; b >= 0; --b) {
+    acc = xyzz_dbl(acc);
+    if ((s.v[b >> 5] >> (b & 31)) & 1u) acc = xyzz_add_affine(acc, gen.x, gen.y);
+  }
+  st_xyzz(&temp[i], acc);
+}
+
+// Batch conversion XYZZ -> affine, one thread per kBatchAff consecutive points
+// (Montgomery's trick on ZZZ; prefix products kept in `pref`).
+__global__ void __launch_bounds__(128) k_batch_affine(const G1xyzz* __restrict__ temp, uint64_t n, Fp* __restrict__ pref,
+                               G1Affine* __restrict__ out, uint8_t* __restrict__ out_inf) {
+  const uint64_t chunk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = chunk * kBatchAff;
+  if (i0 >= n) return;
+  const uint64_t i1 = i0 + kBatchAff < n ? i0 + kBatchAff : n;
+  Fp acc = fe_one<FpCfg>();
+  for (uint64_t i = i0; i < i1; ++i) {
+    G1xyzz p;
+    ld_xyzz(&temp[i], p);
+    if (!xyzz_is_inf(p)) acc = fe_mul(acc, p.ZZZ);
+    st_fp(reinterpret_cast<uint32_t*>(&pref[i]), acc);
+  }
+  Fp inv = fe_inv(acc);
+  for (uint64_t i = i1; i-- > i0;) {
+    G1xyzz p;
+    ld_xyzz(&temp[i], p);
+    if (xyzz_is_inf(p)) {
+      st_aff(&out[i], fe_zero<FpCfg>(), fe_zero<FpCfg>());
+      out_inf[i] = 1;
+      continue;
+    }
+    Fp prev = fe_one<FpCfg>();
+    if (i > i0) ld_fp(reinterpret_cast<const uint32_t*>(&pref[i - 1]), prev);
+    const Fp u = fe_mul(inv, prev);  // 1 / ZZZ_i
+    inv = fe_mul(inv, p.ZZZ);
+    const Fp zzinv = fe_sqr(fe_mul(p.ZZ, u));
+    st_aff(&out[i], fe_mul(p.X, zzinv), fe_mul(p.Y, u));
+    out_inf[i] = 0;
+  }
+}
+
+}  // namespace
+
+// Window size for an SRS of n points (bucket count 2^(c-1); table W*n).
+static uint32_t choose_c(size_t n) {
+  if (n >= (1u << 18)) return 16;
+  if (n >= (1u << 14)) return 13;
+  if (n >= (1u << 10)) return 10;
+  return 8;
+}
+
+int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
+  s->c = choose_c(s->n);
+  s->windows = (256 + s->c - 1) / s->c;
+  const size_t n = s->n;
+  int st;
+  if ((st = s->table.alloc((size_t)s->windows * n * sizeof(G1Affine)))) return st;
+  if ((st = s->table_inf.alloc((size_t)s->windows * n))) return st;
+  PLK_HIP_TRY(hipMemcpyAsync(s->table.ptr, s->points.ptr, n * sizeof(G1Affine),
+                             hipMemcpyDeviceToDevice, stream));
+  PLK_HIP_TRY(hipMemcpyAsync(s->table_inf.ptr, s->inf.ptr, n, hipMemcpyDeviceToDevice, stream));
+  DevBuf temp, pref;
+  if ((st = temp.alloc(n * sizeof(G1xyzz)))) return st;
+  if ((st = pref.alloc(n * sizeof(Fp)))) return st;
+  G1Affine* tab = s->table.as<G1Affine>();
+  uint8_t* tinf = s->table_inf.as<uint8_t>();
+  for (uint32_t w = 1; w < s->windows; ++w) {
+    hipLaunchKernelGGL(k_double_c, dim3(cdiv(n, 256)), dim3(256), 0, stream, tab + (w - 1) * n,
+                       tinf + (w - 1) * n, (uint64_t)n, s->c, temp.as<G1xyzz>());
+    hipLaunchKernelGGL(k_batch_affine, dim3(cdiv(cdiv(n, kBatchAff), 128)), dim3(128), 0, stream,
+                       temp.as<G1xyzz>(), (uint64_t)n, pref.as<Fp>(), tab + w * n, tinf + w * n);
+    PLK_HIP_TRY(hipGetLastError());
+  }
+  PLK_HIP_TRY(hipStreamSynchronize(stream));
+  s->ws.reset(new MsmWorkspace());
+  return ws_reserve(s, n);
+}
+
+int srs_generate(plk_srs* s, const Fr& tau_mont, hipStream_t stream) {
+  const size_t n = s->n;
+  int st;
+  DevBuf temp, pref;
+  if ((st = temp.alloc(n * sizeof(G1xyzz)))) return st;
+  if ((st = pref.alloc(n * sizeof(Fp)))) return st;
+  // G1 generator (Montgomery form)
+  static const uint32_t gx[12] = {0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu,
+                                  0x171bac58u, 0xa14e3a3fu, 0x9774b905u, 0xc3688c4fu,
+                                  0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u};
+  static const uint32_t gy[12] = {0x46c5e7e1u, 0x0caa2329u, 0xa2888ae4u, 0xd03cc744u,
+                                  0x2c04b3edu, 0x00db18cbu, 0xd5d00af6u, 0xfcf5e095u,
+                                  0x741d8ae4u, 0xa09e30edu, 0xe3aaa0f1u, 0x08b3f481u};
+  G1Affine gen;
+  for (int i = 0; i < 12; ++i) {
+    gen.x.v[i] = gx[i];
+    gen.y.v[i] = gy[i];
+  }
+  gen.x = fe_to_mont(gen.x);
+  gen.y = fe_to_mont(gen.y);
+  hipLaunchKernelGGL(k_srs_powers, dim3(cdiv(n, 128)), dim3(128), 0, stream, tau_mont, gen,
+                     (uint64_t)n, temp.as<G1xyzz>());
+  hipLaunchKernelGGL(k_batch_affine, dim3(cdiv(cdiv(n, kBatchAff), 128)), dim3(128), 0, stream,
+                     temp.as<G1xyzz>(), (uint64_t)n, pref.as<Fp>(), s->points.as<G1Affine>(),
+                     s->inf.as<uint8_t>());
+  PLK_HIP_TRY(hipGetLastError());
+  PLK_HIP_TRY(hipStreamSynchronize(stream));
+  return PLK_OK;
+}
+
+}  // namespace plk

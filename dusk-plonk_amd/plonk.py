@@ -1,0 +1,360 @@
+"""Host-side mirror of the reference's hot-path interface, over the C ABI (include/plk.h).
+
+The reference exposes the path through Rust structs of un-vendored crates:
+``poly_commit::Fft`` (new / dft / idft / coset_dft / coset_idft / size / size_inv /
+generator / generator_inv / elements / compute_vanishing_poly_over_coset),
+``Coefficients`` / ``PointsValue`` (``pub Vec<F>`` newtypes), and
+``zksnarks::plonk::PlonkParams`` (setup / trim / commit). This module keeps those names,
+argument meanings and error behaviour:
+
+* NTT calls are infallible for valid lengths and take their input "by value" (a new
+  array is returned, the argument is not modified), as the Rust API moves its ``Vec``.
+* ``PlonkParams.commit`` raises :class:`PlonkError` with ``status == PLK_E_DEGREE`` when
+  the polynomial (trailing zeros ignored) is longer than the trimmed SRS — the only way
+  the reference's ``create_proof`` fails on an unsatisfied circuit (prover.rs:262-265).
+
+Field elements are ``numpy.uint64`` arrays of shape ``[n, 4]`` holding Montgomery-form
+limbs (R = 2^256, exactly the reference's in-memory ``BlsScalar``); G1 points are
+``[n, 13]`` (Montgomery Fp x, y, infinity flag). There is no CPU fallback: without the
+HIP library or a GPU every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parent
+_LIB_PATH = _PKG / "libplk.so"
+
+PLK_OK, PLK_E_DEGREE, PLK_E_ARG, PLK_E_DEVICE, PLK_E_OOM, PLK_E_NODEV = range(6)
+
+# Symbols declared in include/plk.h (checked by tests/test_abi.py)
+ABI_SYMBOLS = (
+    "plk_abi_version", "plk_status_str", "plk_device_count", "plk_ctx_create",
+    "plk_ctx_destroy", "plk_ctx_stream", "plk_ctx_synchronize", "plk_domain_get",
+    "plk_domain_info", "plk_domain_elements", "plk_domain_vanishing_over_coset", "plk_ntt",
+    "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
+    "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
+    "plk_srs_last_msm_stats",
+)
+
+
+class PlonkError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = _lib().plk_status_str(status).decode() if _LIB is not None else str(status)
+        super().__init__(f"{what}: {msg} (status {status})" if what else msg)
+
+
+_LIB = None
+
+
+def _lib():
+    """Load libplk.so (built in-tree by build_ext.py). Fails loudly when absent."""
+    global _LIB
+    if _LIB is None:
+        if not _LIB_PATH.exists():
+            raise ImportError(f"{_LIB_PATH} not built — run __graft_entry__.build() first")
+        lib = C.CDLL(str(_LIB_PATH))
+        vp, u32, u64, sz, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t, C.c_int
+        pp = C.POINTER(C.c_void_p)
+        sig = {
+            "plk_abi_version": (i32, []),
+            "plk_status_str": (C.c_char_p, [i32]),
+            "plk_device_count": (i32, [C.POINTER(i32)]),
+            "plk_ctx_create": (i32, [i32, pp]),
+            "plk_ctx_destroy": (i32, [vp]),
+            "plk_ctx_stream": (i32, [vp, pp]),
+            "plk_ctx_synchronize": (i32, [vp]),
+            "plk_domain_get": (i32, [vp, u32, pp]),
+            "plk_domain_info": (i32, [vp, C.POINTER(u64), vp, vp, vp, vp, vp]),
+            "plk_domain_elements": (i32, [vp, vp]),
+            "plk_domain_vanishing_over_coset": (i32, [vp, u64, vp]),
+            "plk_ntt": (i32, [vp, vp, sz, i32, i32]),
+            "plk_ntt_dev": (i32, [vp, vp, vp, sz, i32, i32, vp, vp]),
+            "plk_ntt_batch_dev": (i32, [vp, vp, sz, i32, i32, vp]),
+            "plk_srs_setup": (i32, [vp, vp, sz, vp, pp]),
+            "plk_srs_load": (i32, [vp, vp, sz, pp]),
+            "plk_srs_destroy": (i32, [vp]),
+            "plk_srs_len": (i32, [vp, C.POINTER(sz)]),
+            "plk_srs_points": (i32, [vp, sz, sz, vp]),
+            "plk_msm": (i32, [vp, vp, sz, vp]),
+            "plk_commit": (i32, [vp, vp, sz, vp]),
+            "plk_commit_dev": (i32, [vp, vp, sz, vp, vp]),
+            "plk_srs_last_msm_stats": (i32, [vp, C.POINTER(C.c_float), C.POINTER(u64),
+                                             C.POINTER(u32)]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        _LIB = lib
+    return _LIB
+
+
+def _check(status: int, what: str):
+    if status != PLK_OK:
+        raise PlonkError(status, what)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(_lib().plk_device_count(C.byref(n)), "plk_device_count")
+    return n.value
+
+
+# ------------------------------------------------------------------------------ context
+class Context:
+    """One plk_ctx per GPU (device memory, stream, cached Fft domains)."""
+
+    _default: dict[int, "Context"] = {}
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(_lib().plk_ctx_create(device, C.byref(h)), "plk_ctx_create")
+        self.handle = h
+        self.device = device
+        self._domains: dict[int, C.c_void_p] = {}
+
+    @classmethod
+    def default(cls, device: int | None = None) -> "Context":
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0")) if "LOCAL_RANK" in os.environ else 0
+            try:
+                import torch  # noqa: F401 — only to follow torch's current device when present
+                if torch.cuda.is_available():
+                    device = torch.cuda.current_device()
+            except Exception:
+                pass
+        if device not in cls._default:
+            cls._default[device] = Context(device)
+        return cls._default[device]
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        _check(_lib().plk_ctx_stream(self.handle, C.byref(s)), "plk_ctx_stream")
+        return s.value or 0
+
+    def synchronize(self):
+        _check(_lib().plk_ctx_synchronize(self.handle), "plk_ctx_synchronize")
+
+    def domain(self, k: int) -> C.c_void_p:
+        if k not in self._domains:
+            d = C.c_void_p()
+            _check(_lib().plk_domain_get(self.handle, k, C.byref(d)), "plk_domain_get")
+            self._domains[k] = d
+        return self._domains[k]
+
+
+# ------------------------------------------------------------------------ value types
+def _as_fr_array(values) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(values, dtype=np.uint64))
+    if a.ndim == 1 and a.size % 4 == 0:
+        a = a.reshape(-1, 4)
+    if a.ndim != 2 or a.shape[1] != 4:
+        raise ValueError("expected uint64[n, 4] Montgomery Fr limbs")
+    return a
+
+
+class Coefficients:
+    """poly_commit::Coefficients<Fr> — ``pub Vec<F>`` of coefficients (``.0`` is ``.values``)."""
+
+    def __init__(self, values):
+        self.values = _as_fr_array(values)
+
+    def __len__(self):
+        return self.values.shape[0]
+
+    def clone(self):
+        return type(self)(self.values.copy())
+
+    def degree(self) -> int:
+        """Index of the last non-zero coefficient (0 for the zero polynomial)."""
+        nz = np.nonzero(self.values.any(axis=1))[0]
+        return int(nz[-1]) if nz.size else 0
+
+
+class PointsValue(Coefficients):
+    """poly_commit::PointsValue<Fr> — evaluations over a domain."""
+
+
+# ------------------------------------------------------------------------------- Fft
+class Fft:
+    """poly_commit::Fft<Fr> on the GPU: ``Fft(k)`` = ``Fft::new(k)`` (n = 2^k).
+
+    w = ROOT_OF_UNITY^(2^(32-k)); cosets use g = 7; tables live in HBM per context.
+    """
+
+    def __init__(self, k: int, ctx: Context | None = None):
+        self.ctx = ctx or Context.default()
+        self.k = k
+        self._d = self.ctx.domain(k)
+        n = C.c_uint64()
+        self._consts = [np.zeros(4, dtype=np.uint64) for _ in range(5)]
+        _check(_lib().plk_domain_info(self._d, C.byref(n), *[_ptr(c) for c in self._consts]),
+               "plk_domain_info")
+        self._n = n.value
+        self._elements = None
+
+    # -- accessors (key.rs:205-207, prover.rs:252,446)
+    def size(self) -> int:
+        return self._n
+
+    def generator(self) -> np.ndarray:
+        return self._consts[0].copy()
+
+    def generator_inv(self) -> np.ndarray:
+        return self._consts[1].copy()
+
+    def size_inv(self) -> np.ndarray:
+        return self._consts[2].copy()
+
+    def coset_generator(self) -> np.ndarray:
+        return self._consts[3].copy()
+
+    @property
+    def elements(self) -> np.ndarray:
+        """elements[i] = w^i (permutation.rs:148)."""
+        if self._elements is None:
+            out = np.zeros((self._n, 4), dtype=np.uint64)
+            _check(_lib().plk_domain_elements(self._d, _ptr(out)), "plk_domain_elements")
+            self._elements = out
+        return self._elements
+
+    def compute_vanishing_poly_over_coset(self, poly_degree: int) -> PointsValue:
+        out = np.zeros((self._n, 4), dtype=np.uint64)
+        _check(_lib().plk_domain_vanishing_over_coset(self._d, poly_degree, _ptr(out)),
+               "plk_domain_vanishing_over_coset")
+        return PointsValue(out)
+
+    # -- transforms
+    def _run(self, vals: np.ndarray, direction: int, coset: int) -> np.ndarray:
+        vals = _as_fr_array(vals)
+        if vals.shape[0] > self._n:
+            raise ValueError(f"input of length {vals.shape[0]} exceeds the domain size {self._n}")
+        buf = np.zeros((self._n, 4), dtype=np.uint64)
+        buf[: vals.shape[0]] = vals
+        _check(_lib().plk_ntt(self._d, _ptr(buf), vals.shape[0], direction, coset), "plk_ntt")
+        return buf
+
+    def dft(self, coeffs: Coefficients) -> PointsValue:
+        return PointsValue(self._run(coeffs.values, 1, 0))
+
+    def idft(self, points: PointsValue) -> Coefficients:
+        return Coefficients(self._run(points.values, -1, 0))
+
+    def coset_dft(self, coeffs: Coefficients) -> PointsValue:
+        return PointsValue(self._run(coeffs.values, 1, 1))
+
+    def coset_idft(self, points: PointsValue) -> Coefficients:
+        return Coefficients(self._run(points.values, -1, 1))
+
+    # -- device-resident variants (torch tensors of dtype int64, shape [n, 4], on cuda)
+    def ntt_dev(self, d_in_ptr: int, d_out_ptr: int, len_in: int, direction: int, coset: bool,
+                stream: int = 0, d_scratch_ptr: int = 0):
+        _check(_lib().plk_ntt_dev(self._d, C.c_void_p(d_in_ptr), C.c_void_p(d_out_ptr), len_in,
+                                  direction, int(coset), C.c_void_p(d_scratch_ptr or None),
+                                  C.c_void_p(stream or None)), "plk_ntt_dev")
+
+
+# ------------------------------------------------------------------------------ KZG
+class Commitment:
+    """Commitment<G1Affine>: one canonical affine point (uint64[13])."""
+
+    def __init__(self, words: np.ndarray):
+        self.words = np.asarray(words, dtype=np.uint64).reshape(13)
+
+    @property
+    def is_identity(self) -> bool:
+        return bool(self.words[12])
+
+    def __eq__(self, other):
+        return isinstance(other, Commitment) and np.array_equal(self.words, other.words)
+
+    def __repr__(self):
+        return "Commitment(identity)" if self.is_identity else \
+            f"Commitment(x0={int(self.words[0]):#x}...)"
+
+
+class PlonkParams:
+    """zksnarks::plonk::PlonkParams<TatePairing> (the G1 side used by the prover).
+
+    ``setup(k, tau)`` restates ``PlonkParams::setup(k, rng)`` with an explicit secret tau
+    (Montgomery Fr limbs) so the CPU and GPU paths see identical randomness; it emits
+    2^k + 8 powers because the blinded z (n+3) and t_4 (up to n+7) overrun 2^k.
+    """
+
+    SLACK = 8
+
+    def __init__(self, handle: C.c_void_p, n_points: int, ctx: Context):
+        self._h = handle
+        self.n = n_points
+        self.ctx = ctx
+
+    @classmethod
+    def setup(cls, k: int, tau, ctx: Context | None = None, n_points: int | None = None):
+        ctx = ctx or Context.default()
+        n = n_points if n_points is not None else (1 << k) + cls.SLACK
+        tau = _as_fr_array(tau).reshape(4)
+        h = C.c_void_p()
+        _check(_lib().plk_srs_setup(ctx.handle, _ptr(tau), n, None, C.byref(h)), "plk_srs_setup")
+        return cls(h, n, ctx)
+
+    @classmethod
+    def load(cls, points: np.ndarray, ctx: Context | None = None):
+        ctx = ctx or Context.default()
+        pts = np.ascontiguousarray(np.asarray(points, dtype=np.uint64).reshape(-1, 13))
+        h = C.c_void_p()
+        _check(_lib().plk_srs_load(ctx.handle, _ptr(pts), pts.shape[0], C.byref(h)), "plk_srs_load")
+        return cls(h, pts.shape[0], ctx)
+
+    def trim(self, n: int) -> "PlonkParams":
+        """Keep the first n + SLACK powers (key.rs:81-82)."""
+        keep = min(self.n, n + self.SLACK)
+        if keep == self.n:
+            return self
+        return PlonkParams.load(self.points(0, keep), self.ctx)
+
+    def points(self, start: int = 0, count: int | None = None) -> np.ndarray:
+        count = self.n - start if count is None else count
+        out = np.zeros((count, 13), dtype=np.uint64)
+        _check(_lib().plk_srs_points(self._h, start, count, _ptr(out)), "plk_srs_points")
+        return out
+
+    def commit(self, poly: Coefficients) -> Commitment:
+        vals = _as_fr_array(poly.values if isinstance(poly, Coefficients) else poly)
+        out = np.zeros(13, dtype=np.uint64)
+        _check(_lib().plk_commit(self._h, _ptr(vals), vals.shape[0], _ptr(out)), "commit")
+        return Commitment(out)
+
+    def msm(self, scalars) -> Commitment:
+        vals = _as_fr_array(scalars)
+        out = np.zeros(13, dtype=np.uint64)
+        _check(_lib().plk_msm(self._h, _ptr(vals), vals.shape[0], _ptr(out)), "msm")
+        return Commitment(out)
+
+    def commit_dev(self, d_ptr: int, length: int, stream: int = 0) -> Commitment:
+        out = np.zeros(13, dtype=np.uint64)
+        _check(_lib().plk_commit_dev(self._h, C.c_void_p(d_ptr), length, _ptr(out),
+                                     C.c_void_p(stream or None)), "commit_dev")
+        return Commitment(out)
+
+    def last_msm_stats(self):
+        ms, adds, c = C.c_float(), C.c_uint64(), C.c_uint32()
+        _check(_lib().plk_srs_last_msm_stats(self._h, C.byref(ms), C.byref(adds), C.byref(c)),
+               "plk_srs_last_msm_stats")
+        return ms.value, adds.value, c.value
+
+    def __del__(self):
+        try:
+            if self._h and _LIB is not None:
+                _LIB.plk_srs_destroy(self._h)
+        except Exception:
+            pass
+        self._h = None

@@ -1,0 +1,148 @@
+"""GPU parity of the NTT family (poly_commit::Fft) through the C ABI.
+
+Bit-exact against the golden fixtures (Python big-int restatement) and the C oracle at
+every size up to 2^16 for all four transforms; size-independent properties (round trips,
+linearity, evaluation at a point) at 2^20 and 2^23 (the 8n domain of n = 2^20).
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import random_fr
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_vectors(plk, gpu_ctx, golden):
+    g = golden["ntt"]
+    for k in (0, 1, 2, 3, 4, 5, 6, 8, 10):
+        f = plk.Fft(k, gpu_ctx)
+        x = plk.Coefficients(g[f"k{k}_in"])
+        assert np.array_equal(f.dft(x).values, g[f"k{k}_dft"]), k
+        assert np.array_equal(f.idft(plk.PointsValue(x.values)).values, g[f"k{k}_idft"]), k
+        assert np.array_equal(f.coset_dft(x).values, g[f"k{k}_coset_dft"]), k
+        assert np.array_equal(f.coset_idft(plk.PointsValue(x.values)).values,
+                              g[f"k{k}_coset_idft"]), k
+        part = plk.Coefficients(g[f"k{k}_part"])
+        assert np.array_equal(f.dft(part).values, g[f"k{k}_part_dft"]), k
+        assert np.array_equal(f.coset_dft(part).values, g[f"k{k}_part_coset_dft"]), k
+        assert np.array_equal(f.elements, g[f"k{k}_elements"]), k
+    f5 = plk.Fft(5, gpu_ctx)
+    assert np.array_equal(f5.compute_vanishing_poly_over_coset(4).values, g["vanish_k5_n4"])
+
+
+@pytest.mark.parametrize("k", list(range(0, 17)))
+def test_all_transforms_vs_oracle(plk, gpu_ctx, oracle, k):
+    n = 1 << k
+    f = plk.Fft(k, gpu_ctx)
+    x = random_fr(n, seed=100 + k)
+    for direction, coset, name in ((1, 0, "dft"), (-1, 0, "idft"), (1, 1, "coset_dft"),
+                                   (-1, 1, "coset_idft")):
+        want = oracle.ntt(x, k, direction, bool(coset))
+        got = getattr(f, name)(plk.Coefficients(x)).values
+        assert np.array_equal(got, want), (k, name)
+    # ragged input, zero padded (len n+2 polys go into 8n domains in the prover)
+    m = max(1, (3 * n) // 4 + 1) if n > 1 else 1
+    assert np.array_equal(f.dft(plk.Coefficients(x[:m])).values, oracle.dft(x[:m], k))
+    assert np.array_equal(f.coset_dft(plk.Coefficients(x[:m])).values, oracle.coset_dft(x[:m], k))
+
+
+def test_empty_and_zero_inputs(plk, gpu_ctx):
+    f = plk.Fft(6, gpu_ctx)
+    z = np.zeros((0, 4), dtype=np.uint64)
+    for fn in (f.dft, f.idft, f.coset_dft, f.coset_idft):
+        assert not fn(plk.Coefficients(z)).values.any()
+    with pytest.raises(ValueError):
+        f.dft(plk.Coefficients(random_fr(65, seed=1)))
+
+
+def test_domain_accessors(plk, gpu_ctx, oracle):
+    import pyref as P
+    for k in (1, 9, 12, 16, 20):
+        f = plk.Fft(k, gpu_ctx)
+        assert f.size() == 1 << k
+        assert P.fr_vec_from_np(f.generator())[0] == P.omega(k)
+        assert P.fr_vec_from_np(f.generator_inv())[0] == pow(P.omega(k), -1, P.R_MOD)
+        assert P.fr_vec_from_np(f.size_inv())[0] == pow(1 << k, -1, P.R_MOD)
+        if k <= 16:
+            assert np.array_equal(f.elements, oracle.elements(k))
+    f = plk.Fft(15, gpu_ctx)
+    assert np.array_equal(f.compute_vanishing_poly_over_coset(1 << 12).values,
+                          oracle.vanishing(15, 1 << 12))
+
+
+def test_sigma_encoding_on_gpu_elements(plk, gpu_ctx):
+    """permutation.rs:913-946: encodings use fft.elements = w^i of the GPU domain."""
+    import pyref as P
+    f = plk.Fft(2, gpu_ctx)
+    el = P.fr_vec_from_np(f.elements)
+    w = P.fr_vec_from_np(f.generator())[0]
+    assert el == [1, w, w * w % P.R_MOD, pow(w, 3, P.R_MOD)]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("k", [18, 20, 23])
+def test_large_properties(plk, gpu_ctx, oracle, k):
+    import pyref as P
+    n = 1 << k
+    f = plk.Fft(k, gpu_ctx)
+    x = random_fr(n, seed=7 + k)
+    y = random_fr(n, seed=8 + k)
+    X = f.dft(plk.Coefficients(x)).values
+    # round trips
+    assert np.array_equal(f.idft(plk.PointsValue(X)).values, x)
+    CX = f.coset_dft(plk.Coefficients(x)).values
+    assert np.array_equal(f.coset_idft(plk.PointsValue(CX)).values, x)
+    # linearity: dft(x + y) == dft(x) + dft(y)  (checked at sampled indices)
+    xs = P.fr_vec_from_np(x[:64])
+    ys = P.fr_vec_from_np(y[:64])
+    s = P.fr_vec_to_np([(a + b) % P.R_MOD for a, b in zip(xs, ys)] + [0] * 0)
+    xy = x.copy()
+    xy[:64] = s
+    xy[64:] = 0
+    xo = x.copy()
+    xo[64:] = 0
+    yo = y.copy()
+    yo[:] = 0
+    yo[:64] = y[:64]
+    D1 = f.dft(plk.Coefficients(xy)).values
+    D2 = f.dft(plk.Coefficients(xo)).values
+    D3 = f.dft(plk.Coefficients(yo)).values
+    idx = np.random.default_rng(k).integers(0, n, 32)
+    for i in idx:
+        a, b, c = (P.fr_vec_from_np(D[i:i + 1])[0] for D in (D1, D2, D3))
+        assert a == (b + c) % P.R_MOD
+    # evaluation: X[i] = x(w^i), CX[i] = x(g w^i) at sampled i (full Horner in Python on a
+    # short prefix polynomial)
+    w = P.omega(k)
+    pre = P.fr_vec_from_np(x[:64])
+    xs_short = x.copy()
+    xs_short[64:] = 0
+    Xs = f.dft(plk.Coefficients(xs_short)).values
+    CXs = f.coset_dft(plk.Coefficients(xs_short)).values
+    for i in idx[:8]:
+        pt = pow(w, int(i), P.R_MOD)
+        assert P.fr_vec_from_np(Xs[i:i + 1])[0] == P.poly_eval(pre, pt)
+        assert P.fr_vec_from_np(CXs[i:i + 1])[0] == P.poly_eval(pre, 7 * pt % P.R_MOD)
+    if k <= 20:  # the C oracle finishes 2^20 in about a second
+        assert np.array_equal(X, oracle.dft(x, k))
+        assert np.array_equal(CX, oracle.coset_dft(x, k))
+
+
+def test_device_entry_points(plk, gpu_ctx, oracle):
+    import torch
+    k = 14
+    n = 1 << k
+    f = plk.Fft(k, gpu_ctx)
+    x = random_fr(n, seed=3)
+    d = torch.from_numpy(x.view(np.int64)).cuda()
+    out = torch.empty_like(d)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    f.ntt_dev(d.data_ptr(), out.data_ptr(), n, 1, True, stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), oracle.coset_dft(x, k))
+    # in place, inverse, with a caller-owned scratch buffer
+    scratch = torch.empty((2 * n, 4), dtype=torch.int64, device="cuda")
+    f.ntt_dev(out.data_ptr(), out.data_ptr(), n, -1, True, stream, scratch.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), x)
