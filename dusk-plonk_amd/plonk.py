@@ -58,6 +58,13 @@ def _lib():
     if _LIB is None:
         if not _LIB_PATH.exists():
             raise ImportError(f"{_LIB_PATH} not built — run __graft_entry__.build() first")
+        # One HIP runtime per process: torch ships its own libamdhip64 (same SONAME as
+        # /opt/rocm's). Loading torch first makes libplk bind to that copy, so device
+        # pointers and hipStream_t handles from torch are valid in our calls.
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
         lib = C.CDLL(str(_LIB_PATH))
         vp, u32, u64, sz, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t, C.c_int
         pp = C.POINTER(C.c_void_p)
