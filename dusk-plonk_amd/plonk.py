@@ -38,7 +38,7 @@ ABI_SYMBOLS = (
     "plk_domain_info", "plk_domain_elements", "plk_domain_vanishing_over_coset", "plk_ntt",
     "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
-    "plk_srs_last_msm_stats",
+    "plk_srs_last_msm_stats", "plk_debug_field_op",
 )
 
 
@@ -93,6 +93,7 @@ def _lib():
             "plk_commit_dev": (i32, [vp, vp, sz, vp, vp]),
             "plk_srs_last_msm_stats": (i32, [vp, C.POINTER(C.c_float), C.POINTER(u64),
                                              C.POINTER(u32)]),
+            "plk_debug_field_op": (i32, [vp, i32, i32, vp, vp, vp, sz]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -150,6 +151,19 @@ class Context:
 
     def synchronize(self):
         _check(_lib().plk_ctx_synchronize(self.handle), "plk_ctx_synchronize")
+
+    def field_op(self, field: str, op: str, a: np.ndarray, b: np.ndarray | None = None):
+        """Elementwise device field arithmetic (test support): field 'fr'|'fp',
+        op 'mul'|'add'|'sub'|'sqr'|'inv'; Montgomery limbs in and out."""
+        w = 4 if field == "fr" else 6
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.uint64).reshape(-1, w))
+        bb = None if b is None else np.ascontiguousarray(np.asarray(b, dtype=np.uint64).reshape(-1, w))
+        out = np.zeros_like(a)
+        code = {"mul": 0, "add": 1, "sub": 2, "sqr": 3, "inv": 4}[op]
+        _check(_lib().plk_debug_field_op(self.handle, 0 if field == "fr" else 1, code, _ptr(a),
+                                         None if bb is None else _ptr(bb), _ptr(out), a.shape[0]),
+               "plk_debug_field_op")
+        return out
 
     def domain(self, k: int) -> C.c_void_p:
         if k not in self._domains:

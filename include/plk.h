@@ -124,6 +124,13 @@ int plk_commit_dev(plk_srs* srs, const plk_fr* d_coeffs, size_t len, plk_g1* out
 int plk_srs_last_msm_stats(const plk_srs* srs, float* accumulate_ms, uint64_t* point_adds,
                            uint32_t* window_bits);
 
+/* ---- test support ---------------------------------------------------------------- */
+/* Elementwise device field arithmetic on host arrays (used by the parity tests to pin the
+ * gfx950 multiplier against the oracle): field 0 = Fr (4 limbs), 1 = Fp (6 limbs);
+ * op 0 = a*b, 1 = a+b, 2 = a-b, 3 = a^2, 4 = a^-1 (Montgomery form in and out). */
+int plk_debug_field_op(plk_ctx* ctx, int field, int op, const uint64_t* a, const uint64_t* b,
+                       uint64_t* out, size_t n);
+
 #ifdef __cplusplus
 }
 #endif
