@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "internal.hpp"
+#include "msm_common.hpp"
 
 using namespace plk;
 
@@ -370,6 +371,32 @@ int plk_commit_dev(plk_srs* s, const plk_fr* d_coeffs, size_t len, plk_g1* out, 
   hipStream_t st = stream ? (hipStream_t)stream : s->ctx->stream;
   const size_t m = len < s->n ? len : s->n;
   return msm_run(s, reinterpret_cast<const Fr*>(d_coeffs), m, len, out, st);
+  PLK_API_END
+}
+
+int plk_commit_batch_dev(plk_srs* s, const plk_fr* const* d_coeffs, const size_t* lens,
+                         size_t count, plk_g1* outs, int* statuses, void* stream) {
+  PLK_API_BEGIN
+  if (!s || !outs || (count && (!d_coeffs || !lens))) return PLK_E_ARG;
+  for (size_t k = 0; k < count; ++k)
+    if (!d_coeffs[k] && lens[k]) return PLK_E_ARG;
+  DeviceGuard g(s->ctx->device);
+  hipStream_t st = stream ? (hipStream_t)stream : s->ctx->stream;
+  int overall = PLK_OK;
+  for (size_t base = 0; base < count; base += kMaxSlots) {
+    const size_t m = count - base < kMaxSlots ? count - base : kMaxSlots;
+    const Fr* ptrs[kMaxSlots];
+    size_t use[kMaxSlots], chk[kMaxSlots];
+    for (size_t k = 0; k < m; ++k) {
+      ptrs[k] = reinterpret_cast<const Fr*>(d_coeffs[base + k]);
+      chk[k] = lens[base + k];
+      use[k] = chk[k] < s->n ? chk[k] : s->n;
+    }
+    const int r = msm_run_batch(s, ptrs, use, chk, m, outs + base, statuses ? statuses + base : nullptr, st);
+    if (r != PLK_OK && r != PLK_E_DEGREE) return r;
+    if (r != PLK_OK && overall == PLK_OK) overall = r;
+  }
+  return overall;
   PLK_API_END
 }
 

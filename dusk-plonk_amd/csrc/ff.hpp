@@ -220,6 +220,19 @@ __device__ __forceinline__ void mac96s(uint64_t& acc, uint32_t& top, uint32_t a,
       : "v"(a), "s"(b));
 }
 
+// one product on each of two independent chains in a single asm block (A: both factors
+// in VGPRs, B: second factor a modulus limb in an SGPR)
+__device__ __forceinline__ void mac96x2(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b,
+                                        uint64_t& acc2, uint32_t& top2, uint32_t a2, uint32_t b2) {
+  uint64_t cy, cy2;
+  asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %2, %5, %8, %9, %2\n\t"
+      "v_addc_co_u32_e64 %1, %4, 0, %1, %4\n\t"
+      "v_addc_co_u32_e64 %3, %5, 0, %3, %5"
+      : "+v"(acc), "+v"(top), "+v"(acc2), "+v"(top2), "=&s"(cy), "=&s"(cy2)
+      : "v"(a), "v"(b), "v"(a2), "s"(b2));
+}
+
 // Montgomery product by columns (FIPS / "Comba-Montgomery"): column k accumulates
 // sum a_i b_{k-i} (chain A) and sum m_i p_{k-i} (chain B, independent of A; the two are
 // interleaved so consecutive v_mad_u64_u32 never depend on each other), then
@@ -240,8 +253,10 @@ __device__ __forceinline__ Fe<C> fe_mul_dev(const Fe<C>& a, const Fe<C>& b) {
     uint32_t topb = 0;
 #pragma unroll
     for (int i = lo_i; i <= hi_a; ++i) {
-      mac96(acc, top, a.v[i], b.v[k - i]);
-      if (i <= hi_m) mac96s(accb, topb, m[i], C::P[k - i]);
+      if (i <= hi_m)
+        mac96x2(acc, top, a.v[i], b.v[k - i], accb, topb, m[i], C::P[k - i]);
+      else
+        mac96(acc, top, a.v[i], b.v[k - i]);
     }
     if (hi_m >= lo_i) {  // merge chain B into A (64-bit add, carry into top)
       const uint64_t sum = acc + accb;

@@ -94,6 +94,7 @@ struct plk_srs {
   std::unique_ptr<plk::MsmWorkspace> ws;
   float last_accumulate_ms = 0.f;
   uint64_t last_point_adds = 0;
+  uint32_t last_slots = 0;
   plk_srs();
   ~plk_srs();
 };
@@ -126,6 +127,9 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
 int msm_prepare_srs(plk_srs* s, hipStream_t stream);
 int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g1* out,
             hipStream_t stream);
+int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
+                  const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
+                  hipStream_t stream);
 void fr_root_of_unity(uint32_t log_n, Fr& omega);
 int ntt_vanishing(plk_domain* d, uint64_t deg, Fr* d_out, hipStream_t s);
 int srs_generate(plk_srs* s, const Fr& tau_mont, hipStream_t stream);

@@ -4,21 +4,27 @@
 // prover.rs:133-136,194,262-265,440,452 and key.rs:138-159).
 //
 // Design (fixed-base Pippenger, all windows folded into one bucket set):
-//  * SRS load: table[w][i] = 2^(c*w) * P_i in affine form, w < W = ceil(256/c). The bases
-//    of a commit are always an SRS prefix, so the table is built once per SRS and kept
-//    resident in HBM (W * n * 96 B: 1.6 GB at n = 2^20, c = 16).
+//  * SRS load (srs.hip): table[w][i] = 2^(c*w) * P_i in affine form, w < W = ceil(256/c),
+//    resident in HBM (W * n * 96 B: 1.6 GB at n = 2^20, c = 16). Commit bases are always
+//    an SRS prefix, so the table is built once.
 //  * Per MSM: each scalar is recoded into W signed c-bit digits |d| <= 2^(c-1); digit
-//    (i, w) sends +-table[w][i] to bucket |d|-1, so there is ONE set of B = 2^(c-1)
-//    buckets and no per-window doubling chain.
-//  * Counting sort by bucket (atomic histogram -> scan -> atomic scatter). Order inside a
-//    bucket is irrelevant: group addition is exact, the canonical affine output is unique.
+//    (i, w) sends +-table[w][i] to bucket |d|-1: ONE set of B = 2^(c-1) buckets and no
+//    per-window doubling chain.
+//  * Counting sort by bucket with a per-CU LDS histogram (B * 4 B <= 128 KiB): LDS atomics
+//    per digit, one coalesced global atomic per (workgroup, bucket) to count and again to
+//    reserve ranges. Order inside a bucket is irrelevant: group addition is exact and the
+//    canonical affine output is unique.
 //  * Bucket accumulation in chunks of CH points (one thread per chunk, XYZZ mixed adds):
-//    the dominant kernel, integer-VALU bound; large buckets (skewed scalars) split evenly.
+//    the dominant kernel, integer-VALU bound.
 //  * Bucket reduction sum_b (b+1) S_b = sum_j 2^j T_j with T_j = sum of the buckets whose
-//    weight has bit j set: two shallow tree kernels produce the c points T_j, and the CPU
-//    runs the 2c-op Horner tail and the single inversion to canonical affine.
+//    weight has bit j set: two shallow tree kernels give the c points T_j and the CPU runs
+//    the 2c-op Horner tail and the single inversion to canonical affine.
+//  * Up to kMaxSlots independent MSMs run as ONE batch (blockIdx.y = slot): the prover's
+//    commits come in independent groups (4 wires, 4 quotient chunks, 2 openings), and the
+//    latency-bound tail kernels of a batch then cost about what one MSM's tail costs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "internal.hpp"
@@ -27,6 +33,8 @@
 namespace plk {
 
 namespace {
+
+constexpr uint32_t kHistThreads = 1024;
 
 // signed c-bit digit w of canonical scalar s (carry threaded through the caller)
 __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, uint32_t c, uint32_t& carry) {
@@ -48,31 +56,56 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, uint32_t c, uin
   return d;
 }
 
-__global__ void k_digits_count(const Fr* __restrict__ scalars, uint64_t len, MsmCfg cfg,
-                               uint32_t* __restrict__ counts) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= len) return;
-  const Fr s = fe_from_mont(ld_fr(&scalars[i]));
-  uint32_t carry = 0;
-  for (uint32_t w = 0; w < cfg.W; ++w) {
-    const int d = digit_at(s, w, cfg.c, carry);
-    if (d != 0) atomicAdd(&counts[(d < 0 ? -d : d) - 1], 1u);
-  }
+__device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t& i1) {
+  const uint32_t per = (len + gridDim.x - 1) / gridDim.x;
+  i0 = blockIdx.x * per;
+  i1 = min(len, i0 + per);
 }
 
-// single workgroup: offsets = exclusive scan(counts), task_off = exclusive scan(ceil(count/CH))
-__global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restrict__ counts, uint32_t B,
+// Pass 1: LDS histogram of this workgroup's digits, flushed to counts[slot][b].
+__global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cfg,
+                                                       uint32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  const uint32_t slot = blockIdx.y, B = cfg.B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  uint32_t i0, i1;
+  slot_range(batch.len[slot], i0, i1);
+  const Fr* sc = batch.scalars[slot];
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const Fr s = fe_from_mont(ld_fr(&sc[i]));
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) {
+      const int d = digit_at(s, w, cfg.c, carry);
+      if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* cnt = counts + (size_t)slot * B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x)
+    if (hist[b]) atomicAdd(&cnt[b], hist[b]);
+}
+
+// single workgroup per slot: offsets = exclusive scan(counts) (also the scatter cursors),
+// task_off = exclusive scan(ceil(count / CH))
+__global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restrict__ counts,
+                                                       uint32_t B, uint32_t chunk,
                                                        uint32_t* __restrict__ offsets,
                                                        uint32_t* __restrict__ task_off,
                                                        uint32_t* __restrict__ cursor) {
   __shared__ uint32_t s_cnt[1024], s_tsk[1024];
+  const uint32_t slot = blockIdx.y;
+  counts += (size_t)slot * B;
+  offsets += (size_t)slot * (B + 1);
+  task_off += (size_t)slot * (B + 1);
+  cursor += (size_t)slot * B;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
   const uint32_t per = (B + nt - 1) / nt;
   const uint32_t b0 = tid * per;
   uint32_t c_sum = 0, t_sum = 0;
   for (uint32_t b = b0; b < b0 + per && b < B; ++b) {
     c_sum += counts[b];
-    t_sum += (counts[b] + kChunk - 1) / kChunk;
+    t_sum += (counts[b] + chunk - 1) / chunk;
   }
   s_cnt[tid] = c_sum;
   s_tsk[tid] = t_sum;
@@ -87,10 +120,10 @@ __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restric
   uint32_t c_run = s_cnt[tid] - c_sum, t_run = s_tsk[tid] - t_sum;
   for (uint32_t b = b0; b < b0 + per && b < B; ++b) {
     offsets[b] = c_run;
+    cursor[b] = c_run;
     task_off[b] = t_run;
-    cursor[b] = 0;
     c_run += counts[b];
-    t_run += (counts[b] + kChunk - 1) / kChunk;
+    t_run += (counts[b] + chunk - 1) / chunk;
   }
   if (tid == nt - 1) {
     offsets[B] = s_cnt[tid];
@@ -98,46 +131,79 @@ __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restric
   }
 }
 
-__global__ void k_digits_scatter(const Fr* __restrict__ scalars, uint64_t len, MsmCfg cfg,
-                                 uint64_t n_srs, const uint32_t* __restrict__ offsets,
-                                 uint32_t* __restrict__ cursor, uint32_t* __restrict__ sorted) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= len) return;
-  const Fr s = fe_from_mont(ld_fr(&scalars[i]));
-  uint32_t carry = 0;
-  for (uint32_t w = 0; w < cfg.W; ++w) {
-    const int d = digit_at(s, w, cfg.c, carry);
-    if (d != 0) {
-      const uint32_t b = (uint32_t)((d < 0 ? -d : d) - 1);
-      const uint32_t pos = offsets[b] + atomicAdd(&cursor[b], 1u);
-      sorted[pos] = (uint32_t)(w * n_srs + i) | (d < 0 ? 0x80000000u : 0u);
+// Pass 2: same histogram again, reserve this workgroup's range of every bucket with one
+// global atomic per bucket, then place each digit with an LDS atomic on the reservation.
+__global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg cfg,
+                                                          uint64_t n_srs,
+                                                          uint32_t* __restrict__ cursor,
+                                                          uint32_t* __restrict__ sorted,
+                                                          uint64_t sorted_stride) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  const uint32_t slot = blockIdx.y, B = cfg.B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  uint32_t i0, i1;
+  slot_range(batch.len[slot], i0, i1);
+  const Fr* sc = batch.scalars[slot];
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const Fr s = fe_from_mont(ld_fr(&sc[i]));
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) {
+      const int d = digit_at(s, w, cfg.c, carry);
+      if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* cur = cursor + (size_t)slot * B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x)
+    if (hist[b]) hist[b] = atomicAdd(&cur[b], hist[b]);
+  __syncthreads();
+  uint32_t* out = sorted + (size_t)slot * sorted_stride;
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const Fr s = fe_from_mont(ld_fr(&sc[i]));
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) {
+      const int d = digit_at(s, w, cfg.c, carry);
+      if (d != 0) {
+        const uint32_t pos = atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+        out[pos] = (uint32_t)(w * n_srs + i) | (d < 0 ? 0x80000000u : 0u);
+      }
     }
   }
 }
 
 // task t of bucket b covers sorted[offsets[b] + t*CH, ...+CH)
-__global__ void k_make_tasks(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ task_off,
-                             uint32_t B, uint2* __restrict__ tasks) {
+__global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
+                             const uint32_t* __restrict__ task_off, uint32_t B, uint32_t chunk,
+                             uint2* __restrict__ tasks, uint64_t task_stride) {
+  const uint32_t slot = blockIdx.y;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  offsets += (size_t)slot * (B + 1);
+  task_off += (size_t)slot * (B + 1);
+  tasks += (size_t)slot * task_stride;
   const uint32_t start = offsets[b], cnt = offsets[b + 1] - start;
   uint32_t t = task_off[b];
-  for (uint32_t o = 0; o < cnt; o += kChunk, ++t) {
-    const uint32_t l = cnt - o < kChunk ? cnt - o : kChunk;
+  for (uint32_t o = 0; o < cnt; o += chunk, ++t) {
+    const uint32_t l = cnt - o < chunk ? cnt - o : chunk;
     tasks[t] = make_uint2(start + o, l);
   }
 }
 
 template <bool HAS_INF>
 __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ tasks,
-                                                    const uint32_t* __restrict__ n_tasks,
+                                                    const uint32_t* __restrict__ task_off,
+                                                    uint32_t B, uint64_t task_stride,
                                                     const uint32_t* __restrict__ sorted,
+                                                    uint64_t sorted_stride,
                                                     const G1Affine* __restrict__ table,
                                                     const uint8_t* __restrict__ table_inf,
                                                     G1xyzz* __restrict__ partials) {
+  const uint32_t slot = blockIdx.y;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= *n_tasks) return;
-  const uint2 task = tasks[t];
+  if (t >= task_off[(size_t)slot * (B + 1) + B]) return;
+  const uint2 task = tasks[(size_t)slot * task_stride + t];
+  sorted += (size_t)slot * sorted_stride;
   G1xyzz acc = xyzz_infinity();
   for (uint32_t e = task.x; e < task.x + task.y; ++e) {
     const uint32_t code = sorted[e];
@@ -148,28 +214,36 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
     if (code & 0x80000000u) y = fe_neg(y);
     acc = xyzz_add_affine(acc, x, y);
   }
-  st_xyzz(&partials[t], acc);
+  st_xyzz(&partials[(size_t)slot * task_stride + t], acc);
 }
 
-__global__ void __launch_bounds__(128) k_bucket_reduce(const uint32_t* __restrict__ task_off, uint32_t B,
-                                const G1xyzz* __restrict__ partials, G1xyzz* __restrict__ buckets) {
+__global__ void __launch_bounds__(128) k_bucket_reduce(const uint32_t* __restrict__ task_off,
+                                                       uint32_t B, uint64_t task_stride,
+                                                       const G1xyzz* __restrict__ partials,
+                                                       G1xyzz* __restrict__ buckets) {
+  const uint32_t slot = blockIdx.y;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  task_off += (size_t)slot * (B + 1);
+  partials += (size_t)slot * task_stride;
   G1xyzz acc = xyzz_infinity();
   for (uint32_t t = task_off[b]; t < task_off[b + 1]; ++t) {
     G1xyzz q;
     ld_xyzz(&partials[t], q);
     acc = xyzz_add(acc, q);
   }
-  st_xyzz(&buckets[b], acc);
+  st_xyzz(&buckets[(size_t)slot * B + b], acc);
 }
 
 // Workgroup g owns buckets [256g, 256g+256). Thread (j, s) sums the 16 buckets
 // 256g + 16s + u whose weight (b+1) has bit j set; then a 16-way LDS tree per j.
-// out[g * nbits + j]
+// out[slot][g * nbits + j]
 __global__ void __launch_bounds__(256) k_bitsum1(const G1xyzz* __restrict__ buckets, uint32_t B,
                                                  uint32_t nbits, G1xyzz* __restrict__ out) {
   __shared__ G1xyzz sh[256];
+  const uint32_t slot = blockIdx.y;
+  buckets += (size_t)slot * B;
+  out += (size_t)slot * gridDim.x * nbits;
   const uint32_t tid = threadIdx.x;
   const uint32_t j = tid >> 4, s = tid & 15;
   G1xyzz acc = xyzz_infinity();
@@ -192,11 +266,12 @@ __global__ void __launch_bounds__(256) k_bitsum1(const G1xyzz* __restrict__ buck
   if (s == 0 && j < nbits) st_xyzz(&out[blockIdx.x * nbits + j], sh[tid]);
 }
 
-// Workgroup j sums in[g * nbits + j] over g < G.
+// Workgroup j of slot sums in[slot][g * nbits + j] over g < G.
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, G1xyzz* __restrict__ out) {
   __shared__ G1xyzz sh[256];
-  const uint32_t tid = threadIdx.x, j = blockIdx.x;
+  const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
+  in += (size_t)slot * G * nbits;
   G1xyzz acc = xyzz_infinity();
   for (uint32_t g = tid; g < G; g += 256) {
     G1xyzz q;
@@ -209,121 +284,179 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
     if (tid < h) sh[tid] = xyzz_add(sh[tid], sh[tid + h]);
     __syncthreads();
   }
-  if (tid == 0) st_xyzz(&out[j], sh[0]);
+  if (tid == 0) st_xyzz(&out[(size_t)slot * nbits + j], sh[0]);
 }
 
-// flags[0] |= any nonzero scalar in [from, to)  (commit degree check)
-__global__ void k_any_nonzero(const Fr* __restrict__ v, uint64_t from, uint64_t to,
-                              uint32_t* __restrict__ flag) {
-  const uint64_t i = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= to) return;
-  if (!fe_is_zero(ld_fr(&v[i]))) atomicOr(flag, 1u);
+// flag[slot] |= any nonzero scalar in [len, check_len)  (commit degree check)
+__global__ void k_any_nonzero(MsmBatch batch, uint32_t* __restrict__ flag) {
+  const uint32_t slot = blockIdx.y;
+  const uint64_t i = (uint64_t)batch.len[slot] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch.check_len[slot]) return;
+  if (!fe_is_zero(ld_fr(&batch.scalars[slot][i]))) atomicOr(&flag[slot], 1u);
 }
 
 }  // namespace
 
-int ws_reserve(plk_srs* s, size_t len) {
+int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
   MsmWorkspace& w = *s->ws;
-  if (len <= w.cap_len && w.cap_len) return PLK_OK;
+  if (len <= w.cap_len && slots <= w.cap_slots && w.cap_len) return PLK_OK;
+  len = std::max(len, w.cap_len);
+  slots = std::max(slots, w.cap_slots);
   const size_t B = (size_t)1 << (s->c - 1);
   const size_t entries = (size_t)s->windows * len;
-  const size_t max_tasks = entries / kChunk + B + 1;
+  const size_t max_tasks = entries / kChunkMin + B + 1;
   const size_t G = (B + 255) / 256;
   int st;
-  if ((st = w.counts.alloc(B * 4))) return st;
-  if ((st = w.offsets.alloc((B + 1) * 4))) return st;
-  if ((st = w.task_off.alloc((B + 1) * 4))) return st;
-  if ((st = w.cursor.alloc(B * 4))) return st;
-  if ((st = w.sorted.alloc(entries * 4 + 4))) return st;
-  if ((st = w.tasks.alloc(max_tasks * sizeof(uint2)))) return st;
-  if ((st = w.partials.alloc(max_tasks * sizeof(G1xyzz)))) return st;
-  if ((st = w.buckets.alloc(B * sizeof(G1xyzz)))) return st;
-  if ((st = w.bits1.alloc(G * s->c * sizeof(G1xyzz)))) return st;
-  if ((st = w.bits2.alloc(s->c * sizeof(G1xyzz)))) return st;
-  if ((st = w.flag.alloc(16))) return st;
+  if ((st = w.counts.alloc(slots * B * 4))) return st;
+  if ((st = w.offsets.alloc(slots * (B + 1) * 4))) return st;
+  if ((st = w.task_off.alloc(slots * (B + 1) * 4))) return st;
+  if ((st = w.cursor.alloc(slots * B * 4))) return st;
+  if ((st = w.sorted.alloc(slots * (entries + 1) * 4))) return st;
+  if ((st = w.tasks.alloc(slots * max_tasks * sizeof(uint2)))) return st;
+  if ((st = w.partials.alloc(slots * max_tasks * sizeof(G1xyzz)))) return st;
+  if ((st = w.buckets.alloc(slots * B * sizeof(G1xyzz)))) return st;
+  if ((st = w.bits1.alloc(slots * G * s->c * sizeof(G1xyzz)))) return st;
+  if ((st = w.bits2.alloc(slots * s->c * sizeof(G1xyzz)))) return st;
+  if ((st = w.flag.alloc(slots * 4 + 16))) return st;
   if (!w.ev0) PLK_HIP_TRY(hipEventCreate(&w.ev0));
   if (!w.ev1) PLK_HIP_TRY(hipEventCreate(&w.ev1));
+  const int lds = (int)(B * 4);
+  PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scatter),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   w.cap_len = len;
+  w.cap_slots = slots;
+  w.task_stride = max_tasks;
+  w.sorted_stride = entries + 1;
   return PLK_OK;
 }
 
-int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g1* out,
-            hipStream_t stream) {
-  if (len > s->n) return PLK_E_ARG;
+// Runs `count` independent MSMs on the same SRS as one batch. For slot k: scalars
+// d_scalars[k][0 .. lens[k]) (lens[k] <= n_srs) against the SRS prefix, and if
+// check_lens[k] > lens[k] the tail [lens[k], check_lens[k]) must be zero (else that slot
+// reports PLK_E_DEGREE). statuses[k] receives each slot's status.
+int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
+                  const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
+                  hipStream_t stream) {
+  if (count == 0) return PLK_OK;
+  if (count > kMaxSlots) return PLK_E_ARG;
+  size_t max_len = 0, max_tail = 0, total_entries = 0;
+  MsmBatch batch{};
+  for (size_t k = 0; k < count; ++k) {
+    if (lens[k] > s->n) return PLK_E_ARG;
+    batch.scalars[k] = d_scalars[k];
+    batch.len[k] = (uint32_t)lens[k];
+    batch.check_len[k] = check_lens ? check_lens[k] : lens[k];
+    max_len = std::max(max_len, lens[k]);
+    if (batch.check_len[k] > lens[k])
+      max_tail = std::max<size_t>(max_tail, batch.check_len[k] - lens[k]);
+    total_entries += (size_t)s->windows * lens[k];
+  }
   int st;
-  if ((st = ws_reserve(s, len ? len : 1))) return st;
+  if ((st = ws_reserve(s, max_len ? max_len : 1, (uint32_t)count))) return st;
   MsmWorkspace& w = *s->ws;
   const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1)};
   const uint32_t B = cfg.B;
   const uint32_t nbits = s->c;  // weights b+1 in [1, 2^(c-1)] need c bits
   const uint32_t G = cdiv(B, 256);
+  const uint32_t slots = (uint32_t)count;
+  // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads
+  const uint32_t chunk = (uint32_t)std::min<size_t>(
+      kChunkMax, std::max<size_t>(kChunkMin, total_entries / 262144));
+  const size_t max_tasks_used = (size_t)s->windows * max_len / chunk + B;
+  const uint32_t hist_blocks = std::max<uint32_t>(1, std::min<uint32_t>(256, cdiv(max_len, 512)));
 
-  PLK_HIP_TRY(hipMemsetAsync(w.flag.ptr, 0, 16, stream));
-  if (check_len > len) {
-    hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(check_len - len, 256)), dim3(256), 0, stream,
-                       d_scalars, (uint64_t)len, (uint64_t)check_len, w.flag.as<uint32_t>());
+  PLK_HIP_TRY(hipMemsetAsync(w.flag.ptr, 0, slots * 4, stream));
+  if (max_tail) {
+    hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
+                       batch, w.flag.as<uint32_t>());
   }
-  PLK_HIP_TRY(hipMemsetAsync(w.counts.ptr, 0, B * 4, stream));
-  if (len) {
-    hipLaunchKernelGGL(k_digits_count, dim3(cdiv(len, 256)), dim3(256), 0, stream, d_scalars,
-                       (uint64_t)len, cfg, w.counts.as<uint32_t>());
+  PLK_HIP_TRY(hipMemsetAsync(w.counts.ptr, 0, (size_t)slots * B * 4, stream));
+  const size_t lds = (size_t)B * 4;
+  if (max_len) {
+    hipLaunchKernelGGL(k_hist, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream, batch,
+                       cfg, w.counts.as<uint32_t>());
   }
-  hipLaunchKernelGGL(k_scan_buckets, dim3(1), dim3(1024), 0, stream, w.counts.as<uint32_t>(), B,
-                     w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.cursor.as<uint32_t>());
-  if (len) {
-    hipLaunchKernelGGL(k_digits_scatter, dim3(cdiv(len, 256)), dim3(256), 0, stream, d_scalars,
-                       (uint64_t)len, cfg, (uint64_t)s->n, w.offsets.as<uint32_t>(),
-                       w.cursor.as<uint32_t>(), w.sorted.as<uint32_t>());
+  hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
+                     w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
+                     w.task_off.as<uint32_t>(), w.cursor.as<uint32_t>());
+  if (max_len) {
+    hipLaunchKernelGGL(k_scatter, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream,
+                       batch, cfg, (uint64_t)s->n, w.cursor.as<uint32_t>(),
+                       w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride);
   }
-  hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256)), dim3(256), 0, stream, w.offsets.as<uint32_t>(),
-                     w.task_off.as<uint32_t>(), B, w.tasks.as<uint2>());
-  const size_t max_tasks = (size_t)s->windows * len / kChunk + B;
+  hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
+                     w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), B, chunk,
+                     w.tasks.as<uint2>(), (uint64_t)w.task_stride);
   PLK_HIP_TRY(hipEventRecord(w.ev0, stream));
   if (s->has_inf) {
-    hipLaunchKernelGGL(k_accumulate<true>, dim3(cdiv(max_tasks, 256)), dim3(256), 0, stream,
-                       w.tasks.as<uint2>(), w.task_off.as<uint32_t>() + B, w.sorted.as<uint32_t>(),
-                       s->table.as<G1Affine>(), s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
+    hipLaunchKernelGGL(k_accumulate<true>, dim3(cdiv(max_tasks_used, 256), slots), dim3(256), 0,
+                       stream, w.tasks.as<uint2>(), w.task_off.as<uint32_t>(), B,
+                       (uint64_t)w.task_stride, w.sorted.as<uint32_t>(),
+                       (uint64_t)w.sorted_stride, s->table.as<G1Affine>(),
+                       s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
   } else {
-    hipLaunchKernelGGL(k_accumulate<false>, dim3(cdiv(max_tasks, 256)), dim3(256), 0, stream,
-                       w.tasks.as<uint2>(), w.task_off.as<uint32_t>() + B, w.sorted.as<uint32_t>(),
-                       s->table.as<G1Affine>(), s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
+    hipLaunchKernelGGL(k_accumulate<false>, dim3(cdiv(max_tasks_used, 256), slots), dim3(256), 0,
+                       stream, w.tasks.as<uint2>(), w.task_off.as<uint32_t>(), B,
+                       (uint64_t)w.task_stride, w.sorted.as<uint32_t>(),
+                       (uint64_t)w.sorted_stride, s->table.as<G1Affine>(),
+                       s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
   }
   PLK_HIP_TRY(hipEventRecord(w.ev1, stream));
-  hipLaunchKernelGGL(k_bucket_reduce, dim3(cdiv(B, 128)), dim3(128), 0, stream,
-                     w.task_off.as<uint32_t>(), B, w.partials.as<G1xyzz>(), w.buckets.as<G1xyzz>());
-  hipLaunchKernelGGL(k_bitsum1, dim3(G), dim3(256), 0, stream, w.buckets.as<G1xyzz>(), B, nbits,
-                     w.bits1.as<G1xyzz>());
-  hipLaunchKernelGGL(k_bitsum2, dim3(nbits), dim3(256), 0, stream, w.bits1.as<G1xyzz>(), G, nbits,
-                     w.bits2.as<G1xyzz>());
+  hipLaunchKernelGGL(k_bucket_reduce, dim3(cdiv(B, 128), slots), dim3(128), 0, stream,
+                     w.task_off.as<uint32_t>(), B, (uint64_t)w.task_stride,
+                     w.partials.as<G1xyzz>(), w.buckets.as<G1xyzz>());
+  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, w.buckets.as<G1xyzz>(), B,
+                     nbits, w.bits1.as<G1xyzz>());
+  hipLaunchKernelGGL(k_bitsum2, dim3(nbits, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
+                     G, nbits, w.bits2.as<G1xyzz>());
   PLK_HIP_TRY(hipGetLastError());
 
-  std::vector<G1xyzz> T(nbits);
-  uint32_t flag = 0, entries = 0;
-  PLK_HIP_TRY(hipMemcpyAsync(&entries, w.offsets.as<uint32_t>() + B, 4, hipMemcpyDeviceToHost,
-                             stream));
-  PLK_HIP_TRY(hipMemcpyAsync(T.data(), w.bits2.ptr, nbits * sizeof(G1xyzz), hipMemcpyDeviceToHost,
-                             stream));
-  PLK_HIP_TRY(hipMemcpyAsync(&flag, w.flag.ptr, 4, hipMemcpyDeviceToHost, stream));
+  std::vector<G1xyzz> T((size_t)slots * nbits);
+  std::vector<uint32_t> flag(slots), ent(slots);
+  PLK_HIP_TRY(hipMemcpy2DAsync(ent.data(), 4, w.offsets.as<uint32_t>() + B, (B + 1) * 4, 4, slots,
+                               hipMemcpyDeviceToHost, stream));
+  PLK_HIP_TRY(hipMemcpyAsync(T.data(), w.bits2.ptr, T.size() * sizeof(G1xyzz),
+                             hipMemcpyDeviceToHost, stream));
+  PLK_HIP_TRY(hipMemcpyAsync(flag.data(), w.flag.ptr, slots * 4, hipMemcpyDeviceToHost, stream));
   PLK_HIP_TRY(hipStreamSynchronize(stream));
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, w.ev0, w.ev1) == hipSuccess) s->last_accumulate_ms = ms;
-  s->last_point_adds = entries;  // nonzero digits = mixed adds in k_accumulate
-  if (flag) return PLK_E_DEGREE;
+  s->last_point_adds = 0;
+  for (uint32_t k = 0; k < slots; ++k) s->last_point_adds += ent[k];
+  s->last_slots = slots;
 
-  // host tail: sum_j 2^j T_j (Horner), then canonical affine
-  G1xyzz acc = xyzz_infinity();
-  for (int j = (int)nbits - 1; j >= 0; --j) {
-    acc = xyzz_dbl(acc);
-    acc = xyzz_add(acc, T[j]);
+  int overall = PLK_OK;
+  for (uint32_t k = 0; k < slots; ++k) {
+    plk_g1* out = &outs[k];
+    if (flag[k]) {
+      *out = plk_g1{};
+      if (statuses) statuses[k] = PLK_E_DEGREE;
+      if (overall == PLK_OK) overall = PLK_E_DEGREE;
+      continue;
+    }
+    // host tail: sum_j 2^j T_j (Horner), then canonical affine
+    G1xyzz acc = xyzz_infinity();
+    for (int j = (int)nbits - 1; j >= 0; --j) {
+      acc = xyzz_dbl(acc);
+      acc = xyzz_add(acc, T[(size_t)k * nbits + j]);
+    }
+    Fp x, y;
+    const bool fin = xyzz_to_affine(acc, x, y);
+    for (int i = 0; i < 6; ++i) {
+      out->x[i] = (uint64_t)x.v[2 * i] | ((uint64_t)x.v[2 * i + 1] << 32);
+      out->y[i] = (uint64_t)y.v[2 * i] | ((uint64_t)y.v[2 * i + 1] << 32);
+    }
+    out->infinity = fin ? 0 : 1;
+    if (statuses) statuses[k] = PLK_OK;
   }
-  Fp x, y;
-  const bool fin = xyzz_to_affine(acc, x, y);
-  for (int i = 0; i < 6; ++i) {
-    out->x[i] = (uint64_t)x.v[2 * i] | ((uint64_t)x.v[2 * i + 1] << 32);
-    out->y[i] = (uint64_t)y.v[2 * i] | ((uint64_t)y.v[2 * i + 1] << 32);
-  }
-  out->infinity = fin ? 0 : 1;
-  return PLK_OK;
+  return overall;
+}
+
+int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g1* out,
+            hipStream_t stream) {
+  return msm_run_batch(s, &d_scalars, &len, &check_len, 1, out, nullptr, stream);
 }
 
 }  // namespace plk

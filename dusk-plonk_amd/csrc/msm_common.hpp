@@ -4,11 +4,20 @@
 
 namespace plk {
 
-constexpr uint32_t kChunk = 64;     // points per accumulation task
+constexpr uint32_t kChunkMin = 16;  // points per accumulation task (bounds)
+constexpr uint32_t kChunkMax = 64;
 constexpr uint32_t kBatchAff = 32;  // points per batch-inversion chunk
+constexpr uint32_t kMaxSlots = 16;  // independent MSMs per batch
 
 struct MsmCfg {
   uint32_t c, W, B;
+};
+
+// Kernel-argument view of one batch of independent MSMs (slot = blockIdx.y).
+struct MsmBatch {
+  const Fr* scalars[kMaxSlots];
+  uint32_t len[kMaxSlots];
+  uint64_t check_len[kMaxSlots];
 };
 
 __device__ __forceinline__ void ld_fp(const uint32_t* p, Fp& r) {
@@ -60,7 +69,8 @@ inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b
 
 struct MsmWorkspace {
   DevBuf counts, offsets, task_off, cursor, sorted, tasks, partials, buckets, bits1, bits2, flag;
-  size_t cap_len = 0;
+  size_t cap_len = 0, task_stride = 0, sorted_stride = 0;
+  uint32_t cap_slots = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   ~MsmWorkspace() {
     if (ev0) (void)hipEventDestroy(ev0);
@@ -68,6 +78,6 @@ struct MsmWorkspace {
   }
 };
 
-int ws_reserve(plk_srs* s, size_t len);
+int ws_reserve(plk_srs* s, size_t len, uint32_t slots);
 
 }  // namespace plk

@@ -113,7 +113,7 @@ int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   }
   PLK_HIP_TRY(hipStreamSynchronize(stream));
   s->ws.reset(new MsmWorkspace());
-  return ws_reserve(s, n);
+  return ws_reserve(s, n, 1);
 }
 
 int srs_generate(plk_srs* s, const Fr& tau_mont, hipStream_t stream) {

@@ -38,7 +38,7 @@ ABI_SYMBOLS = (
     "plk_domain_info", "plk_domain_elements", "plk_domain_vanishing_over_coset", "plk_ntt",
     "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
-    "plk_srs_last_msm_stats", "plk_debug_field_op",
+    "plk_srs_last_msm_stats", "plk_debug_field_op", "plk_commit_batch_dev",
 )
 
 
@@ -94,6 +94,7 @@ def _lib():
             "plk_srs_last_msm_stats": (i32, [vp, C.POINTER(C.c_float), C.POINTER(u64),
                                              C.POINTER(u32)]),
             "plk_debug_field_op": (i32, [vp, i32, i32, vp, vp, vp, sz]),
+            "plk_commit_batch_dev": (i32, [vp, vp, vp, sz, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -365,6 +366,21 @@ class PlonkParams:
         _check(_lib().plk_commit_dev(self._h, C.c_void_p(d_ptr), length, _ptr(out),
                                      C.c_void_p(stream or None)), "commit_dev")
         return Commitment(out)
+
+    def commit_batch_dev(self, ptrs_lens, stream: int = 0, raise_on_error: bool = True):
+        """Commit several device-resident polynomials [(ptr, len), ...] as one batch.
+        Returns a list of Commitment (or PlonkError per failed slot when not raising)."""
+        k = len(ptrs_lens)
+        ptrs = (C.c_void_p * k)(*[C.c_void_p(p) for p, _ in ptrs_lens])
+        lens = (C.c_size_t * k)(*[n for _, n in ptrs_lens])
+        outs = np.zeros((k, 13), dtype=np.uint64)
+        sts = (C.c_int * k)()
+        st = _lib().plk_commit_batch_dev(self._h, ptrs, lens, k, _ptr(outs), sts,
+                                         C.c_void_p(stream or None))
+        if st not in (PLK_OK, PLK_E_DEGREE) or (raise_on_error and st != PLK_OK):
+            raise PlonkError(st, "commit_batch_dev")
+        return [Commitment(outs[i]) if sts[i] == PLK_OK else PlonkError(sts[i], "commit")
+                for i in range(k)]
 
     def last_msm_stats(self):
         ms, adds, c = C.c_float(), C.c_uint64(), C.c_uint32()

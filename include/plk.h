@@ -117,6 +117,14 @@ int plk_commit(plk_srs* srs, const plk_fr* coeffs, size_t len, plk_g1* out);
 int plk_commit_dev(plk_srs* srs, const plk_fr* d_coeffs, size_t len, plk_g1* out,
                    void* stream);
 
+/* Batched device commit: `count` independent polynomials (d_coeffs[k], lens[k]) committed
+ * as one GPU batch (their kernels share launches; the latency-bound reduction tails of the
+ * batch overlap). Used for the prover's independent commit groups: the 4 wire commits
+ * (prover.rs:133-136), the 4 quotient chunks (:262-265) and the 2 openings (:440,452).
+ * statuses (nullable) gets each commit's status; returns PLK_E_DEGREE if any failed. */
+int plk_commit_batch_dev(plk_srs* srs, const plk_fr* const* d_coeffs, const size_t* lens,
+                         size_t count, plk_g1* outs, int* statuses, void* stream);
+
 /* ---- instrumentation (bench / profiling) ------------------------------------------- */
 /* Milliseconds of the dominant kernel of the most recent plk_commit/plk_msm on this SRS
  * (bucket accumulation), measured with HIP events on the launching stream; and the

@@ -130,3 +130,31 @@ def test_msm_2_20_properties(plk, gpu_ctx):
         e = np.zeros((i + 1, 4), dtype=np.uint64)
         e[i] = fr_int(1)[0]
         assert np.array_equal(pp.commit(plk.Coefficients(e)).words[:12], pp.points(i, 1)[0, :12])
+
+
+def test_commit_batch_dev(plk, gpu_ctx, oracle):
+    """Independent commits as one batch (the prover's wire / quotient / opening groups):
+    different lengths, a zero polynomial, and one slot past the SRS (degree error)."""
+    import torch
+    n = 1 << 11
+    pp = plk.PlonkParams.setup(11, random_fr(1, seed=31)[0], gpu_ctx, n_points=n + 8)
+    pts = pp.points()
+    lens = [n, n + 3, 17, n // 2, 1, n + 8]
+    polys = [random_fr(m, seed=40 + i) for i, m in enumerate(lens)]
+    polys[4][:] = 0  # zero polynomial -> identity
+    bad = random_fr(n + 20, seed=99)  # longer than the SRS with a non-zero tail
+    devs = [torch.from_numpy(p.view(np.int64)).cuda() for p in polys + [bad]]
+    torch.cuda.synchronize()
+    res = pp.commit_batch_dev([(d.data_ptr(), d.shape[0]) for d in devs],
+                              torch.cuda.current_stream().cuda_stream, raise_on_error=False)
+    for i, p in enumerate(polys):
+        assert np.array_equal(res[i].words, oracle.msm(pts[: p.shape[0]], p)), i
+    assert isinstance(res[-1], plk.PlonkError) and res[-1].status == plk.PLK_E_DEGREE
+    # more than one batch worth of slots (>16) goes through in chunks
+    many = [random_fr(64, seed=200 + i) for i in range(20)]
+    dm = [torch.from_numpy(p.view(np.int64)).cuda() for p in many]
+    torch.cuda.synchronize()
+    out = pp.commit_batch_dev([(d.data_ptr(), 64) for d in dm],
+                              torch.cuda.current_stream().cuda_stream)
+    for i, p in enumerate(many):
+        assert np.array_equal(out[i].words, oracle.msm(pts[:64], p)), i

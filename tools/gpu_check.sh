@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m "gpu and not slow" -x -q -p no:cacheprovider > gpurun_out/t2.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/t2.log; exit 1; }
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/t2.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/t2.log; exit 1; }
 tail -3 gpurun_out/t2.log
 timeout -k 10 120 ./tools/ubench > gpurun_out/ubench.log 2>&1 || { echo UBENCH_FAILED; cat gpurun_out/ubench.log; exit 1; }
 cat gpurun_out/ubench.log
