@@ -267,6 +267,11 @@ static int srs_finish(plk_srs* s) {
 
 int plk_srs_setup(plk_ctx* ctx, const plk_fr* tau, size_t n_points, plk_g1* out_points,
                   plk_srs** out) {
+  return plk_srs_setup_range(ctx, tau, 0, n_points, out_points, out);
+}
+
+int plk_srs_setup_range(plk_ctx* ctx, const plk_fr* tau, uint64_t start, size_t n_points,
+                        plk_g1* out_points, plk_srs** out) {
   PLK_API_BEGIN
   if (!ctx || !tau || !out || n_points == 0 || n_points > (1ull << 26)) return PLK_E_ARG;
   *out = nullptr;
@@ -274,7 +279,7 @@ int plk_srs_setup(plk_ctx* ctx, const plk_fr* tau, size_t n_points, plk_g1* out_
   std::unique_ptr<plk_srs> s;
   int st;
   if ((st = srs_alloc(ctx, n_points, s))) return st;
-  if ((st = srs_generate(s.get(), fr_from_abi(tau), ctx->stream))) return st;
+  if ((st = srs_generate(s.get(), fr_from_abi(tau), start, ctx->stream))) return st;
   if ((st = srs_finish(s.get()))) return st;
   if (out_points && (st = plk_srs_points(s.get(), 0, n_points, out_points))) return st;
   *out = s.release();
@@ -397,6 +402,28 @@ int plk_commit_batch_dev(plk_srs* s, const plk_fr* const* d_coeffs, const size_t
     if (r != PLK_OK && overall == PLK_OK) overall = r;
   }
   return overall;
+  PLK_API_END
+}
+
+int plk_g1_sum(const plk_g1* points, size_t n, plk_g1* out) {
+  PLK_API_BEGIN
+  if (!out || (!points && n)) return PLK_E_ARG;
+  G1xyzz acc = xyzz_infinity();
+  for (size_t i = 0; i < n; ++i) {
+    if (points[i].infinity) continue;
+    Fp x, y;
+    for (int k = 0; k < 6; ++k) {
+      x.v[2 * k] = (uint32_t)points[i].x[k];
+      x.v[2 * k + 1] = (uint32_t)(points[i].x[k] >> 32);
+      y.v[2 * k] = (uint32_t)points[i].y[k];
+      y.v[2 * k + 1] = (uint32_t)(points[i].y[k] >> 32);
+    }
+    acc = xyzz_add_affine(acc, x, y);
+  }
+  G1Affine r;
+  const bool fin = xyzz_to_affine(acc, r.x, r.y);
+  g1_to_abi(r, fin ? 0 : 1, out);
+  return PLK_OK;
   PLK_API_END
 }
 

@@ -132,5 +132,5 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
                   hipStream_t stream);
 void fr_root_of_unity(uint32_t log_n, Fr& omega);
 int ntt_vanishing(plk_domain* d, uint64_t deg, Fr* d_out, hipStream_t s);
-int srs_generate(plk_srs* s, const Fr& tau_mont, hipStream_t stream);
+int srs_generate(plk_srs* s, const Fr& tau_mont, uint64_t start, hipStream_t stream);
 }  // namespace plk

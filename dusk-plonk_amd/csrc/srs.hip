@@ -33,10 +33,11 @@ __global__ void __launch_bounds__(256) k_double_c(const G1Affine* __restrict__ s
 }
 
 // temp[i] = [tau^i] G  (XYZZ), double-and-add on the canonical exponent
-__global__ void __launch_bounds__(128) k_srs_powers(Fr tau, G1Affine gen, uint64_t n, G1xyzz* __restrict__ temp) {
+__global__ void __launch_bounds__(128) k_srs_powers(Fr tau, G1Affine gen, uint64_t start, uint64_t n,
+                                                   G1xyzz* __restrict__ temp) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const Fr s = fe_from_mont(fe_pow_u64(tau, i));
+  const Fr s = fe_from_mont(fe_pow_u64(tau, start + i));
   G1xyzz acc = xyzz_infinity();
   for (int b = 254; b >= 0; --b) {
     acc = xyzz_dbl(acc);
@@ -116,7 +117,7 @@ int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   return ws_reserve(s, n, 1);
 }
 
-int srs_generate(plk_srs* s, const Fr& tau_mont, hipStream_t stream) {
+int srs_generate(plk_srs* s, const Fr& tau_mont, uint64_t start, hipStream_t stream) {
   const size_t n = s->n;
   int st;
   DevBuf temp, pref;
@@ -137,7 +138,7 @@ int srs_generate(plk_srs* s, const Fr& tau_mont, hipStream_t stream) {
   gen.x = fe_to_mont(gen.x);
   gen.y = fe_to_mont(gen.y);
   hipLaunchKernelGGL(k_srs_powers, dim3(cdiv(n, 128)), dim3(128), 0, stream, tau_mont, gen,
-                     (uint64_t)n, temp.as<G1xyzz>());
+                     start, (uint64_t)n, temp.as<G1xyzz>());
   hipLaunchKernelGGL(k_batch_affine, dim3(cdiv(cdiv(n, kBatchAff), 128)), dim3(128), 0, stream,
                      temp.as<G1xyzz>(), (uint64_t)n, pref.as<Fp>(), s->points.as<G1Affine>(),
                      s->inf.as<uint8_t>());

@@ -39,6 +39,7 @@ ABI_SYMBOLS = (
     "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
     "plk_srs_last_msm_stats", "plk_debug_field_op", "plk_commit_batch_dev",
+    "plk_srs_setup_range", "plk_g1_sum",
 )
 
 
@@ -95,6 +96,8 @@ def _lib():
                                              C.POINTER(u32)]),
             "plk_debug_field_op": (i32, [vp, i32, i32, vp, vp, vp, sz]),
             "plk_commit_batch_dev": (i32, [vp, vp, vp, sz, vp, vp, vp]),
+            "plk_srs_setup_range": (i32, [vp, vp, u64, sz, vp, pp]),
+            "plk_g1_sum": (i32, [vp, sz, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -304,6 +307,14 @@ class Commitment:
             f"Commitment(x0={int(self.words[0]):#x}...)"
 
 
+def g1_sum(points: np.ndarray) -> Commitment:
+    """Host-side sum of affine points uint64[n, 13] (no GPU needed)."""
+    pts = np.ascontiguousarray(np.asarray(points, dtype=np.uint64).reshape(-1, 13))
+    out = np.zeros(13, dtype=np.uint64)
+    _check(_lib().plk_g1_sum(_ptr(pts), pts.shape[0], _ptr(out)), "plk_g1_sum")
+    return Commitment(out)
+
+
 class PlonkParams:
     """zksnarks::plonk::PlonkParams<TatePairing> (the G1 side used by the prover).
 
@@ -327,6 +338,16 @@ class PlonkParams:
         h = C.c_void_p()
         _check(_lib().plk_srs_setup(ctx.handle, _ptr(tau), n, None, C.byref(h)), "plk_srs_setup")
         return cls(h, n, ctx)
+
+    @classmethod
+    def setup_range(cls, tau, start: int, count: int, ctx: Context | None = None):
+        """The slice [start, start + count) of the SRS of `tau` (a sharded MSM's shard)."""
+        ctx = ctx or Context.default()
+        tau = _as_fr_array(tau).reshape(4)
+        h = C.c_void_p()
+        _check(_lib().plk_srs_setup_range(ctx.handle, _ptr(tau), start, count, None, C.byref(h)),
+               "plk_srs_setup_range")
+        return cls(h, count, ctx)
 
     @classmethod
     def load(cls, points: np.ndarray, ctx: Context | None = None):

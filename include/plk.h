@@ -99,6 +99,10 @@ int plk_ntt_batch_dev(plk_domain* d, plk_fr* d_inout, size_t count, int dir, int
  * points are also copied to the host. The returned SRS is resident and MSM-ready. */
 int plk_srs_setup(plk_ctx* ctx, const plk_fr* tau, size_t n_points, plk_g1* out_points,
                   plk_srs** out);
+/* The slice [start, start + n_points) of the same SRS (g1[i] = [tau^i]G1 for i in the
+ * range): the per-GPU shard of a sharded MSM. */
+int plk_srs_setup_range(plk_ctx* ctx, const plk_fr* tau, uint64_t start, size_t n_points,
+                        plk_g1* out_points, plk_srs** out);
 /* Load an existing SRS (e.g. a trimmed PlonkParams) from host affine points. */
 int plk_srs_load(plk_ctx* ctx, const plk_g1* points, size_t n_points, plk_srs** out);
 int plk_srs_destroy(plk_srs* srs);
@@ -124,6 +128,10 @@ int plk_commit_dev(plk_srs* srs, const plk_fr* d_coeffs, size_t len, plk_g1* out
  * statuses (nullable) gets each commit's status; returns PLK_E_DEGREE if any failed. */
 int plk_commit_batch_dev(plk_srs* srs, const plk_fr* const* d_coeffs, const size_t* lens,
                          size_t count, plk_g1* outs, int* statuses, void* stream);
+
+/* Host-side sum of n affine points (canonical affine out): the local fold after the RCCL
+ * all-gather of per-GPU partial commitments of a sharded MSM. Needs no GPU. */
+int plk_g1_sum(const plk_g1* points, size_t n, plk_g1* out);
 
 /* ---- instrumentation (bench / profiling) ------------------------------------------- */
 /* Milliseconds of the dominant kernel of the most recent plk_commit/plk_msm on this SRS

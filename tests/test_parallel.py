@@ -1,0 +1,142 @@
+"""Multi-process tests of the sharded single MSM.
+
+CPU (gloo, world_size 2): shard ranges, the all-gather of per-rank partial points and the
+host fold (plk_g1_sum, no GPU needed) are the product code; the per-rank partial MSM is
+computed by the C oracle (test infrastructure) since this container has no GPU.
+GPU: two ranks on one card run the real path (SRS shards on the GPU, commits on the GPU,
+gather over gloo) against the unsharded commit.
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_range_partitions():
+    sys.path.insert(0, str(ROOT))
+    from dusk_plonk_amd.parallel import shard_range
+    for n in (1, 7, 64, 1000, (1 << 20) + 8):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_g1_sum_host(plk, oracle, golden):
+    g = golden["msm"]
+    srs = g["srs"]
+    ones = np.tile(np.asarray(__import__("pyref").fr_vec_to_np([1])[0]), (srs.shape[0], 1))
+    assert np.array_equal(plk.plonk.g1_sum(srs).words, oracle.msm(srs, ones))
+    assert plk.plonk.g1_sum(srs[:0]).is_identity
+    # P + (-P) = identity
+    neg = srs[:1].copy()
+    import pyref as P
+    x, y = P.g1_vec_from_np(neg)[0]
+    both = P.g1_vec_to_np([(x, y), (x, (-y) % P.P_MOD)])
+    assert plk.plonk.g1_sum(both).is_identity
+
+
+def _cpu_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import torch.distributed as dist
+    import oracle_lib
+    from dusk_plonk_amd.parallel import gather_fold, shard_range
+    import dusk_plonk_amd as plk
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        orc = oracle_lib.load()
+        g = dict(np.load(ROOT / "tests" / "golden" / "msm_golden.npz", allow_pickle=False))
+        srs = g["srs"]
+        n = srs.shape[0]
+        lo, hi = shard_range(n, world, rank)
+        slots = ["random", "sparse", "minus_one"]
+        parts = np.stack([orc.msm(srs[lo:hi], g[f"{s}_scalars"][lo:hi]) for s in slots])
+        res = gather_fold(parts, [plk.PLK_OK] * len(slots))
+        ok = all(np.array_equal(r.words, g[f"{s}_result"]) for r, s in zip(res, slots))
+        # a degree error on one rank is seen by every rank
+        st = [plk.PLK_OK, plk.PLK_E_DEGREE if rank == world - 1 else plk.PLK_OK, plk.PLK_OK]
+        res2 = gather_fold(parts, st)
+        ok &= isinstance(res2[1], plk.PlonkError) and res2[1].status == plk.PLK_E_DEGREE
+        ok &= np.array_equal(res2[0].words, g["random_result"])
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(fn, world, *args):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q, *args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    out = dict(q.get(timeout=5) for _ in range(world))
+    for p in procs:
+        assert p.exitcode == 0
+    return out
+
+
+def test_sharded_msm_gather_fold_gloo_world2():
+    out = _spawn(_cpu_worker, 2)
+    assert out == {0: True, 1: True}
+
+
+def _gpu_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import torch
+    import torch.distributed as dist
+    from oracle_lib import random_fr
+    import dusk_plonk_amd as plk
+    from dusk_plonk_amd.parallel import ShardedPlonkParams
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        k = 12
+        tau = random_fr(1, seed=77)[0]
+        ctx = plk.Context.default(0)
+        sh = ShardedPlonkParams(k, tau, ctx=ctx)
+        full = plk.PlonkParams.setup(k, tau, ctx)
+        n = (1 << k) + 8
+        polys = [random_fr(m, seed=300 + i) for i, m in enumerate([n, n - 5, 33, 1 << k])]
+        devs = [torch.from_numpy(p.view(np.int64)).cuda() for p in polys]
+        bad = torch.from_numpy(random_fr(n + 40, seed=9).view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        s = torch.cuda.current_stream().cuda_stream
+        res = sh.commit_batch_dev([(d.data_ptr(), d.shape[0]) for d in devs] +
+                                  [(bad.data_ptr(), bad.shape[0])], s)
+        ok = all(np.array_equal(r.words, full.commit(plk.Coefficients(p)).words)
+                 for r, p in zip(res, polys))
+        ok &= isinstance(res[-1], plk.PlonkError) and res[-1].status == plk.PLK_E_DEGREE
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_commit_two_ranks_one_gpu(plk, gpu_ctx):
+    out = _spawn(_gpu_worker, 2)
+    assert out == {0: True, 1: True}
