@@ -1,0 +1,871 @@
+// prover.hip — host orchestration of the PLONK prover on the GPU: the composer (restating
+// the reference's Plonk<C>, /root/reference/src/lib.rs), PlonkKey::compile_with_circuit
+// (src/key.rs:63-327) and Prover::create_proof (src/prover.rs:67-474), with every O(n)
+// step on the device (ntt.hip, msm.hip, prover_kernels.hip) and only the transcript and
+// O(1) scalar algebra on the host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "internal.hpp"
+#include "msm_common.hpp"
+#include "prover.hpp"
+#include "transcript.hpp"
+
+using namespace plk;
+
+namespace {
+
+Fr fr_u64(uint64_t v) {
+  Fr x = fe_zero<FrCfg>();
+  x.v[0] = (uint32_t)v;
+  x.v[1] = (uint32_t)(v >> 32);
+  return fe_to_mont(x);
+}
+Fr fr_from(const plk_fr& a) {
+  Fr r;
+  for (int i = 0; i < 4; ++i) {
+    r.v[2 * i] = (uint32_t)a.l[i];
+    r.v[2 * i + 1] = (uint32_t)(a.l[i] >> 32);
+  }
+  return r;
+}
+plk_fr fr_to(const Fr& a) {
+  plk_fr r;
+  for (int i = 0; i < 4; ++i) r.l[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
+  return r;
+}
+bool fr_eq(const Fr& a, const Fr& b) { return fe_eq(a, b); }
+
+// SplitMix64 -> uniform Fr (4 words, top masked to 255 bits, rejection), Montgomery out.
+// The prover's randomness (blinding scalars) comes from an explicit seed so the CPU and
+// GPU paths can consume identical randomness (SURVEY §7 hard part 5).
+struct Rng {
+  uint64_t s;
+  uint64_t next() {
+    s += 0x9E3779B97F4A7C15ull;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  Fr fr() {
+    for (;;) {
+      Fr c;
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t w = next();
+        c.v[2 * i] = (uint32_t)w;
+        c.v[2 * i + 1] = (uint32_t)(w >> 32);
+      }
+      c.v[7] &= 0x7fffffffu;
+      bool lt = false;
+      for (int i = 7; i >= 0; --i)
+        if (c.v[i] != FrCfg::P[i]) {
+          lt = c.v[i] < FrCfg::P[i];
+          break;
+        }
+      if (lt) return fe_to_mont(c);
+    }
+  }
+};
+
+enum { QM = 0, QL, QR, QO, Q4, QC, QARITH, QRANGE, QLOGIC, QFIXED, QVAR };
+
+Gate default_gate() {
+  Gate g;
+  for (auto& q : g.q) q = fe_zero<FrCfg>();
+  for (auto& w : g.w) w = 0;  // Plonk::ZERO
+  g.has_pi = false;
+  g.pi = fe_zero<FrCfg>();
+  return g;
+}
+
+uint32_t append_witness(plk_composer* c, const Fr& v) {
+  c->witness.push_back(v);
+  c->wire_map.emplace_back();
+  return (uint32_t)(c->witness.size() - 1);
+}
+
+int append_custom_gate(plk_composer* c, const Gate& g) {
+  for (int k = 0; k < 4; ++k)
+    if (g.w[k] >= c->witness.size()) return PLK_E_ARG;  // permutation.rs:98 assert
+  const uint32_t n = (uint32_t)c->gates.size();
+  c->gates.push_back(g);
+  for (int k = 0; k < 4; ++k) c->wire_map[g.w[k]].push_back(4 * n + k);
+  return PLK_OK;
+}
+
+int append_gate(plk_composer* c, Gate g) {  // Constraint::arithmetic
+  g.q[QARITH] = fe_one<FrCfg>();
+  return append_custom_gate(c, g);
+}
+
+// append_evaluated_output (lib.rs:555-600): o = -(q_m a b + q_l a + q_r b + q_4 d + q_c + PI) / q_o
+bool evaluated_output(plk_composer* c, const Gate& s, uint32_t& out) {
+  const Fr a = c->witness[s.w[0]], b = c->witness[s.w[1]], d = c->witness[s.w[3]];
+  Fr x = fe_mul(fe_mul(s.q[QM], a), b);
+  x = fe_add(x, fe_mul(s.q[QL], a));
+  x = fe_add(x, fe_mul(s.q[QR], b));
+  x = fe_add(x, fe_mul(s.q[Q4], d));
+  x = fe_add(x, s.q[QC]);
+  if (s.has_pi) x = fe_add(x, s.pi);
+  const Fr y = s.q[QO];
+  if (fe_is_zero(y)) return false;
+  Fr o;
+  if (fr_eq(y, fe_one<FrCfg>()))
+    o = fe_neg(x);
+  else if (fr_eq(y, fe_neg(fe_one<FrCfg>())))
+    o = x;
+  else
+    o = fe_mul(x, fe_neg(fe_inv(y)));
+  out = append_witness(c, o);
+  return true;
+}
+
+void assert_equal_constant(plk_composer* c, uint32_t a, const Fr& constant, const Fr* pi) {
+  Gate g = default_gate();
+  g.q[QL] = fe_one<FrCfg>();
+  g.q[QC] = fe_neg(constant);
+  g.w[0] = a;
+  if (pi) {
+    g.has_pi = true;
+    g.pi = *pi;
+  }
+  (void)append_gate(c, g);
+}
+
+// lib.rs:606-640
+void append_dummy_gates(plk_composer* c) {
+  const uint32_t six = append_witness(c, fr_u64(6));
+  const uint32_t one = append_witness(c, fr_u64(1));
+  const uint32_t seven = append_witness(c, fr_u64(7));
+  const uint32_t min_twenty = append_witness(c, fe_neg(fr_u64(20)));
+  Gate g = default_gate();
+  g.q[QM] = fr_u64(1);
+  g.q[QL] = fr_u64(2);
+  g.q[QR] = fr_u64(3);
+  g.q[Q4] = fr_u64(1);
+  g.q[QC] = fr_u64(4);
+  g.q[QO] = fr_u64(4);
+  g.w[0] = six;
+  g.w[1] = seven;
+  g.w[3] = one;
+  g.w[2] = min_twenty;
+  (void)append_gate(c, g);
+  Gate h = default_gate();
+  h.q[QM] = fr_u64(1);
+  h.q[QL] = fr_u64(1);
+  h.q[QR] = fr_u64(1);
+  h.q[QC] = fr_u64(127);
+  h.q[QO] = fr_u64(1);
+  h.w[0] = min_twenty;
+  h.w[1] = six;
+  h.w[2] = seven;
+  (void)append_gate(c, h);
+}
+
+Gate gate_from(const plk_constraint* s) {
+  Gate g = default_gate();
+  const plk_fr* qs[11] = {&s->q_m, &s->q_l, &s->q_r, &s->q_o, &s->q_4, &s->q_c, &s->q_arith,
+                          &s->q_range, &s->q_logic, &s->q_fixed_group_add, &s->q_variable_group_add};
+  for (int i = 0; i < 11; ++i) g.q[i] = fr_from(*qs[i]);
+  g.w[0] = s->a;
+  g.w[1] = s->b;
+  g.w[2] = s->o;
+  g.w[3] = s->d;
+  g.has_pi = s->has_public != 0;
+  g.pi = fr_from(s->public_input);
+  return g;
+}
+
+uint32_t log2_ceil(uint64_t x) {
+  uint32_t k = 0;
+  while ((1ull << k) < x) ++k;
+  return k;
+}
+
+#define TRY(...)                       \
+  do {                                 \
+    int _st = (__VA_ARGS__);           \
+    if (_st != PLK_OK) return _st;     \
+  } while (0)
+
+// commit a batch of device polys against the key's trimmed SRS (key.rs:81-82): a poly whose
+// non-zero part is longer than the trimmed SRS fails with PLK_E_DEGREE.
+int key_commit(plk_key* key, const std::vector<const Fr*>& ptrs, const std::vector<size_t>& lens,
+               plk_g1* outs, int* statuses, hipStream_t s) {
+  const size_t max_points = std::min<size_t>(key->srs->n, key->n_trim);
+  std::vector<size_t> use(lens.size());
+  for (size_t i = 0; i < lens.size(); ++i) use[i] = std::min(lens[i], max_points);
+  int overall = PLK_OK;
+  for (size_t base = 0; base < ptrs.size(); base += kMaxSlots) {
+    const size_t m = std::min<size_t>(kMaxSlots, ptrs.size() - base);
+    const int r = msm_run_batch(key->srs, ptrs.data() + base, use.data() + base, lens.data() + base,
+                                m, outs + base, statuses ? statuses + base : nullptr, s);
+    if (r != PLK_OK && r != PLK_E_DEGREE) return r;
+    if (r != PLK_OK) overall = r;
+  }
+  return overall;
+}
+
+Fr d2h_fr(const Fr* p, hipStream_t s) {
+  Fr v;
+  (void)hipMemcpyAsync(&v, p, sizeof(Fr), hipMemcpyDeviceToHost, s);
+  (void)hipStreamSynchronize(s);
+  return v;
+}
+
+}  // namespace
+
+// sigma values k_col(next) * w^gate(next) from wire codes (4*gate + col)
+namespace plk {
+namespace {
+__global__ void k_sigma_values(const uint32_t* __restrict__ codes, const Fr* __restrict__ el,
+                               uint64_t n, Fr k1, Fr k2, Fr k3, Fr* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * n) return;
+  const uint32_t code = codes[i];
+  const uint32_t g = code >> 2, col = code & 3;
+  Fr v = el[g];
+  if (col == 1) v = fe_mul(v, k1);
+  if (col == 2) v = fe_mul(v, k2);
+  if (col == 3) v = fe_mul(v, k3);
+  out[i] = v;
+}
+}  // namespace
+}  // namespace plk
+
+extern "C" {
+
+// ----------------------------------------------------------------------- composer
+int plk_composer_create(plk_composer** out) {
+  try {
+    if (!out) return PLK_E_ARG;
+    std::unique_ptr<plk_composer> c(new plk_composer());
+    // Plonk::initialize (lib.rs:121-134)
+    const uint32_t zero = append_witness(c.get(), fe_zero<FrCfg>());
+    const uint32_t one = append_witness(c.get(), fe_one<FrCfg>());
+    assert_equal_constant(c.get(), zero, fe_zero<FrCfg>(), nullptr);
+    assert_equal_constant(c.get(), one, fe_one<FrCfg>(), nullptr);
+    append_dummy_gates(c.get());
+    append_dummy_gates(c.get());
+    *out = c.release();
+    return PLK_OK;
+  } catch (...) {
+    return PLK_E_OOM;
+  }
+}
+
+int plk_composer_destroy(plk_composer* c) {
+  delete c;
+  return PLK_OK;
+}
+
+int plk_composer_size(const plk_composer* c, size_t* gates, size_t* witnesses) {
+  if (!c) return PLK_E_ARG;
+  if (gates) *gates = c->gates.size();
+  if (witnesses) *witnesses = c->witness.size();
+  return PLK_OK;
+}
+
+int plk_composer_append_witness(plk_composer* c, const plk_fr* v, uint32_t* wire) {
+  if (!c || !v || !wire) return PLK_E_ARG;
+  *wire = append_witness(c, fr_from(*v));
+  return PLK_OK;
+}
+
+int plk_composer_witness_value(const plk_composer* c, uint32_t wire, plk_fr* v) {
+  if (!c || !v || wire >= c->witness.size()) return PLK_E_ARG;
+  *v = fr_to(c->witness[wire]);
+  return PLK_OK;
+}
+
+// lib.rs:708-719: witness + assert_equal_constant(w, 0, Some(-public))
+int plk_composer_append_public(plk_composer* c, const plk_fr* v, uint32_t* wire) {
+  if (!c || !v || !wire) return PLK_E_ARG;
+  const Fr val = fr_from(*v);
+  *wire = append_witness(c, val);
+  const Fr neg = fe_neg(val);
+  assert_equal_constant(c, *wire, fe_zero<FrCfg>(), &neg);
+  return PLK_OK;
+}
+
+int plk_composer_append_gate(plk_composer* c, const plk_constraint* s) {
+  if (!c || !s) return PLK_E_ARG;
+  return append_gate(c, gate_from(s));
+}
+
+int plk_composer_append_custom_gate(plk_composer* c, const plk_constraint* s) {
+  if (!c || !s) return PLK_E_ARG;
+  return append_custom_gate(c, gate_from(s));
+}
+
+// lib.rs:1169-1197: q_o = -1, o := evaluated output, append
+int plk_composer_gate_eval(plk_composer* c, const plk_constraint* s, uint32_t* out) {
+  if (!c || !s || !out) return PLK_E_ARG;
+  Gate g = gate_from(s);
+  g.q[QARITH] = fe_one<FrCfg>();
+  g.q[QO] = fe_neg(fe_one<FrCfg>());
+  for (int k = 0; k < 4; ++k)
+    if (g.w[k] >= c->witness.size() && k != 2) return PLK_E_ARG;
+  uint32_t o;
+  if (!evaluated_output(c, g, o)) return PLK_E_ARG;
+  g.w[2] = o;
+  *out = o;
+  return append_gate(c, g);
+}
+
+int plk_composer_assert_equal(plk_composer* c, uint32_t a, uint32_t b) {
+  if (!c || a >= c->witness.size() || b >= c->witness.size()) return PLK_E_ARG;
+  Gate g = default_gate();  // lib.rs:721-730
+  g.q[QL] = fe_one<FrCfg>();
+  g.q[QR] = fe_neg(fe_one<FrCfg>());
+  g.w[0] = a;
+  g.w[1] = b;
+  return append_gate(c, g);
+}
+
+int plk_composer_assert_equal_constant(plk_composer* c, uint32_t a, const plk_fr* constant,
+                                       const plk_fr* public_input) {
+  if (!c || !constant || a >= c->witness.size()) return PLK_E_ARG;
+  const Fr pi = public_input ? fr_from(*public_input) : fe_zero<FrCfg>();
+  assert_equal_constant(c, a, fr_from(*constant), public_input ? &pi : nullptr);
+  return PLK_OK;
+}
+
+int plk_composer_component_boolean(plk_composer* c, uint32_t a) {
+  if (!c || a >= c->witness.size()) return PLK_E_ARG;
+  Gate g = default_gate();  // lib.rs:859-872
+  g.q[QM] = fe_one<FrCfg>();
+  g.q[QO] = fe_neg(fe_one<FrCfg>());
+  g.w[0] = a;
+  g.w[1] = a;
+  g.w[2] = a;
+  g.w[3] = 0;
+  return append_gate(c, g);
+}
+
+// The bench circuit: `gates` arithmetic gates of the chain
+// x_{i+1} = x_i * y_i + x_i via gate_mul-style gates (q_m = 1, q_l = 1, q_o = -1) whose
+// outputs feed the next gate's a-wire (non-trivial copy constraints); y_i from SplitMix64.
+int plk_composer_synthetic_chain(plk_composer* c, size_t gates, uint64_t seed) {
+  if (!c) return PLK_E_ARG;
+  try {
+    Rng rng{seed};
+    uint32_t x = append_witness(c, rng.fr());
+    c->witness.reserve(c->witness.size() + 2 * gates);
+    c->wire_map.reserve(c->wire_map.size() + 2 * gates);
+    c->gates.reserve(c->gates.size() + gates);
+    const Fr one = fe_one<FrCfg>();
+    for (size_t i = 0; i < gates; ++i) {
+      const uint32_t y = append_witness(c, rng.fr());
+      Gate g = default_gate();
+      g.q[QM] = one;
+      g.q[QL] = one;
+      g.q[QARITH] = one;
+      g.q[QO] = fe_neg(one);
+      g.w[0] = x;
+      g.w[1] = y;
+      const Fr o = fe_add(fe_mul(c->witness[x], c->witness[y]), c->witness[x]);
+      g.w[2] = append_witness(c, o);
+      if (append_custom_gate(c, g) != PLK_OK) return PLK_E_ARG;
+      x = g.w[2];
+    }
+    return PLK_OK;
+  } catch (...) {
+    return PLK_E_OOM;
+  }
+}
+
+// Overwrite witness values (a new instance of the same circuit, as create_proof
+// re-synthesizes the circuit with new witnesses, prover.rs:76-78).
+int plk_composer_set_witness(plk_composer* c, uint32_t wire, const plk_fr* v) {
+  if (!c || !v || wire >= c->witness.size()) return PLK_E_ARG;
+  c->witness[wire] = fr_from(*v);
+  return PLK_OK;
+}
+
+// public inputs, sorted by gate index (Plonk::instance, lib.rs:182-196)
+int plk_composer_public_inputs(const plk_composer* c, plk_fr* values, uint64_t* indexes,
+                               size_t cap, size_t* count) {
+  if (!c || !count) return PLK_E_ARG;
+  size_t k = 0;
+  for (size_t i = 0; i < c->gates.size(); ++i) {
+    if (!c->gates[i].has_pi) continue;
+    if (k < cap) {
+      if (values) values[k] = fr_to(c->gates[i].pi);
+      if (indexes) indexes[k] = i;
+    }
+    ++k;
+  }
+  *count = k;
+  return PLK_OK;
+}
+
+// ---------------------------------------------------------------------------- key
+int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk_key** out) {
+  try {
+    if (!srs || !cs || !out) return PLK_E_ARG;
+    *out = nullptr;
+    plk_ctx* ctx = srs->ctx;
+    DeviceGuard guard(ctx->device);
+    hipStream_t s = ctx->stream;
+    std::unique_ptr<plk_key> key(new plk_key());
+    key->ctx = ctx;
+    key->srs = srs;
+    key->label = label ? label : "plonk";
+    const uint64_t m = cs->gates.size();
+    const uint32_t k = log2_ceil(m);
+    const uint64_t n = 1ull << k;
+    key->m = m;
+    key->n = n;
+    key->k = k;
+    key->gates = cs->gates;
+    // keypair.trim(additional_n) with additional_n = next_pow2(m + 6) (key.rs:81-82); the
+    // trimmed SRS keeps PlonkParams' slack of 8 points
+    key->n_trim = (1ull << log2_ceil(m + 6)) + 8;
+    if (k + 3 > 27) return PLK_E_ARG;
+    for (const Gate& g : cs->gates) {
+      if (!fe_is_zero(g.q[QLOGIC]) || !fe_is_zero(g.q[QFIXED]) || !fe_is_zero(g.q[QVAR]))
+        return PLK_E_UNSUPPORTED;  // logic / curve widgets: next round
+      if (!fe_is_zero(g.q[QRANGE])) key->has_range = true;
+    }
+    TRY(plk_domain_get(ctx, k, &key->dom));
+    TRY(plk_domain_get(ctx, k + 3, &key->dom8));
+    const uint64_t n8 = 8 * n;
+
+    // 1. selectors padded to n (key.rs:89-119) -> idft (key.rs:121-131)
+    std::vector<Fr> host(11 * n, fe_zero<FrCfg>());
+    for (uint64_t i = 0; i < m; ++i)
+      for (int q = 0; q < 11; ++q) host[q * n + i] = cs->gates[i].q[q];
+    TRY(key->q_coef.alloc(11 * n * sizeof(Fr)));
+    PLK_HIP_TRY(hipMemcpyAsync(key->q_coef.ptr, host.data(), 11 * n * sizeof(Fr),
+                               hipMemcpyHostToDevice, s));
+    Fr* qc = key->q_coef.as<Fr>();
+    for (int q = 0; q < 11; ++q) TRY(ntt_run(key->dom, qc + q * n, qc + q * n, n, -1, 0, nullptr, s, 1));
+
+    // 2. sigma permutations (permutation.rs:108-141) and Lagrange encodings (:143-168)
+    std::vector<uint32_t> codes(4 * n);
+    for (uint64_t i = 0; i < n; ++i)
+      for (uint32_t col = 0; col < 4; ++col) codes[col * n + i] = (uint32_t)(4 * i + col);
+    for (const auto& wires : cs->wire_map)
+      for (size_t j = 0; j < wires.size(); ++j) {
+        const uint32_t cur = wires[j], nxt = wires[(j + 1) % wires.size()];
+        codes[(cur & 3) * n + (cur >> 2)] = nxt;
+      }
+    DevBuf dcodes;
+    TRY(dcodes.alloc(4 * n * 4));
+    PLK_HIP_TRY(hipMemcpyAsync(dcodes.ptr, codes.data(), 4 * n * 4, hipMemcpyHostToDevice, s));
+    TRY(key->sigma_lag.alloc(4 * n * sizeof(Fr)));
+    hipLaunchKernelGGL(k_sigma_values, dim3((unsigned)((4 * n + 255) / 256)), dim3(256), 0, s,
+                       dcodes.as<uint32_t>(), key->dom->tw_fwd.as<Fr>(), n, fr_u64(7), fr_u64(13),
+                       fr_u64(17), key->sigma_lag.as<Fr>());
+    PLK_HIP_TRY(hipGetLastError());
+    TRY(key->sigma_coef.alloc(4 * n * sizeof(Fr)));
+    Fr* sc = key->sigma_coef.as<Fr>();
+    for (int c = 0; c < 4; ++c)
+      TRY(ntt_run(key->dom, key->sigma_lag.as<Fr>() + c * n, sc + c * n, n, -1, 0, nullptr, s, 1));
+
+    // 3. commitments (key.rs:138-159): selectors swallow errors, sigmas propagate
+    const int order[11] = {QM, QL, QR, QO, QC, Q4, QARITH, QRANGE, QLOGIC, QFIXED, QVAR};
+    std::vector<const Fr*> ptrs;
+    std::vector<size_t> lens;
+    for (int q : order) {
+      ptrs.push_back(qc + q * n);
+      lens.push_back(n);
+    }
+    for (int c = 0; c < 4; ++c) {
+      ptrs.push_back(sc + c * n);
+      lens.push_back(n);
+    }
+    int sts[15];
+    const int r = key_commit(key.get(), ptrs, lens, key->comms, sts, s);
+    if (r != PLK_OK && r != PLK_E_DEGREE) return r;
+    for (int i = 0; i < 11; ++i)
+      if (sts[i] != PLK_OK) key->comms[i] = plk_g1{{0}, {0}, 1};  // unwrap_or_default
+    for (int i = 11; i < 15; ++i)
+      if (sts[i] != PLK_OK) return sts[i];
+
+    // 4. 8n coset evaluations (key.rs:220-245) and v_h over the coset (key.rs:291)
+    TRY(key->sel8.alloc(SEL_COUNT8 * n8 * sizeof(Fr)));
+    const int sel_src[SEL_COUNT8] = {QM, QL, QR, QO, Q4, QC, QARITH, QRANGE};
+    for (int j = 0; j < SEL_COUNT8; ++j)
+      TRY(ntt_run(key->dom8, qc + sel_src[j] * n, key->sel8.as<Fr>() + j * n8, n, 1, 1, nullptr, s, 1));
+    TRY(key->sigma8.alloc(4 * n8 * sizeof(Fr)));
+    for (int c = 0; c < 4; ++c)
+      TRY(ntt_run(key->dom8, sc + c * n, key->sigma8.as<Fr>() + c * n8, n, 1, 1, nullptr, s, 1));
+    // v_h[i] = (g w8^i)^n - 1 has period 8: invert the 8 values once
+    const Fr gn = fe_pow_u64(key->dom8->g, n), wn = fe_pow_u64(key->dom8->omega, n);
+    Fr x = gn;
+    for (int j = 0; j < 8; ++j) {
+      key->vh_inv[j] = fe_inv(fe_sub(x, fe_one<FrCfg>()));
+      x = fe_mul(x, wn);
+    }
+    // 5. wire indices for the per-proof gather (prover.rs:114-119)
+    std::vector<uint32_t> idx(4 * n, 0);
+    for (uint64_t i = 0; i < m; ++i)
+      for (int c = 0; c < 4; ++c) idx[c * n + i] = cs->gates[i].w[c];
+    TRY(key->wire_idx.alloc(4 * n * 4));
+    PLK_HIP_TRY(hipMemcpyAsync(key->wire_idx.ptr, idx.data(), 4 * n * 4, hipMemcpyHostToDevice, s));
+    PLK_HIP_TRY(hipStreamSynchronize(s));
+    *out = key.release();
+    return PLK_OK;
+  } catch (const std::bad_alloc&) {
+    return PLK_E_OOM;
+  } catch (...) {
+    return PLK_E_DEVICE;
+  }
+}
+
+int plk_key_destroy(plk_key* key) {
+  if (!key) return PLK_E_ARG;
+  DeviceGuard g(key->ctx->device);
+  (void)hipStreamSynchronize(key->ctx->stream);
+  delete key;
+  return PLK_OK;
+}
+
+int plk_key_info(const plk_key* key, uint64_t* n, uint64_t* m, plk_g1* commitments) {
+  if (!key) return PLK_E_ARG;
+  if (n) *n = key->n;
+  if (m) *m = key->m;
+  if (commitments) std::memcpy(commitments, key->comms, sizeof key->comms);
+  return PLK_OK;
+}
+
+// ----------------------------------------------------------------------- prover
+int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* proof,
+              plk_fr* public_inputs, size_t pi_cap, size_t* pi_count) {
+  try {
+    if (!key || !cs || !proof) return PLK_E_ARG;
+    if (cs->gates.size() != key->m) return PLK_E_ARG;
+    DeviceGuard guard(key->ctx->device);
+    hipStream_t s = key->ctx->stream;
+    const uint64_t n = key->n, m = key->m, n8 = 8 * n, S = n + 8;  // S: padded poly stride
+    Rng rng{seed};
+    const Fr one = fe_one<FrCfg>();
+    const Fr K1 = fr_u64(7), K2 = fr_u64(13), K3 = fr_u64(17);
+
+    // scratch (allocated once per key)
+    TRY(key->witness.alloc(std::max<size_t>(cs->witness.size(), 1) * sizeof(Fr)));
+    TRY(key->wires_lag.alloc(4 * n * sizeof(Fr)));
+    TRY(key->wires_coef.alloc(4 * S * sizeof(Fr)));
+    TRY(key->z_lag.alloc(n * sizeof(Fr)));
+    TRY(key->z_coef.alloc(S * sizeof(Fr)));
+    TRY(key->num.alloc(n * sizeof(Fr)));
+    TRY(key->den.alloc(n * sizeof(Fr)));
+    TRY(key->scan_tmp.alloc((pk_scan_tmp_elems(5 * n) + 1) * sizeof(Fr)));
+    TRY(key->pi_lag.alloc(n * sizeof(Fr)));
+    TRY(key->pi_coef.alloc(n * sizeof(Fr)));
+    TRY(key->ev8.alloc(7 * n8 * sizeof(Fr)));
+    TRY(key->quot8.alloc(n8 * sizeof(Fr)));
+    TRY(key->t_coef.alloc(n8 * sizeof(Fr)));
+    TRY(key->r_coef.alloc(S * sizeof(Fr)));
+    TRY(key->agg.alloc(5 * n * sizeof(Fr)));
+    TRY(key->agg2.alloc(S * sizeof(Fr)));
+    TRY(key->w_coef.alloc((5 * n + S) * sizeof(Fr)));
+    TRY(key->tmp_a.alloc(5 * n * sizeof(Fr)));
+    TRY(key->eval_partial.alloc((size_t)kMaxEval * pk_eval_max_blocks(n8) * sizeof(Fr)));
+    TRY(key->eval_out.alloc(kMaxEval * sizeof(Fr)));
+
+    // transcript seeded like Prover::new (prover.rs:54-55): Transcript::base(label, vk, m)
+    Transcript tr(key->label);
+    {
+      const char dom[] = "circuit_size";
+      tr.append_message("dom-sep", reinterpret_cast<const uint8_t*>(dom), sizeof(dom) - 1);
+      tr.append_u64("n", m);
+      const char* labels[15] = {"q_m", "q_l", "q_r", "q_o", "q_c", "q_4", "q_arith", "q_range",
+                                "q_logic", "q_fixed_group_add", "q_variable_group_add",
+                                "s_sigma_1", "s_sigma_2", "s_sigma_3", "s_sigma_4"};
+      for (int i = 0; i < 15; ++i) tr.append_commitment(labels[i], key->comms[i]);
+    }
+    // public inputs (prover.rs:90-105)
+    std::vector<std::pair<uint64_t, Fr>> pis;
+    for (uint64_t i = 0; i < m; ++i)
+      if (cs->gates[i].has_pi) pis.emplace_back(i, cs->gates[i].pi);
+    for (auto& p : pis) tr.append_scalar("pi", p.second);
+    if (pi_count) *pi_count = pis.size();
+    if (public_inputs)
+      for (size_t i = 0; i < pis.size() && i < pi_cap; ++i) public_inputs[i] = fr_to(pis[i].second);
+
+    // ---- round 1: wires -> idft -> blind(1) -> commit (prover.rs:107-158)
+    PLK_HIP_TRY(hipMemcpyAsync(key->witness.ptr, cs->witness.data(), cs->witness.size() * sizeof(Fr),
+                               hipMemcpyHostToDevice, s));
+    Fr* wl = key->wires_lag.as<Fr>();
+    Fr* wc = key->wires_coef.as<Fr>();
+    TRY(pk_gather_wires(key->witness.as<Fr>(), key->wire_idx.as<uint32_t>(), m, n, wl, s));
+    for (int c = 0; c < 4; ++c) {
+      TRY(ntt_run(key->dom, wl + c * n, wc + c * S, n, -1, 0, nullptr, s, 1));
+      BlindArgs b{};
+      b.count = 2;
+      b.r[0] = rng.fr();
+      b.r[1] = rng.fr();
+      TRY(pk_blind(wc + c * S, n, b, s));
+    }
+    plk_g1 wcom[4];
+    TRY(key_commit(key, {wc, wc + S, wc + 2 * S, wc + 3 * S}, {n + 2, n + 2, n + 2, n + 2}, wcom,
+                   nullptr, s));
+    tr.append_commitment("a_w", wcom[0]);
+    tr.append_commitment("b_w", wcom[1]);
+    tr.append_commitment("c_w", wcom[2]);
+    tr.append_commitment("d_w", wcom[3]);
+
+    // ---- round 2: permutation grand product z (prover.rs:160-199)
+    const Fr beta = tr.challenge_scalar("beta");
+    tr.append_scalar("beta", beta);
+    const Fr gamma = tr.challenge_scalar("gamma");
+    Fr* num = key->num.as<Fr>();
+    Fr* den = key->den.as<Fr>();
+    TRY(pk_perm_numden(wl, key->sigma_lag.as<Fr>(), key->dom->tw_fwd.as<Fr>(), n, beta, gamma, K1,
+                       K2, K3, num, den, s));
+    Fr* st = key->scan_tmp.as<Fr>();
+    TRY(pk_scan(num, num, n, true, false, true, st, s));   // N_i = prod_{j<i} num_j
+    TRY(pk_scan(den, den, n, true, true, false, st, s));   // S_i = prod_{j>=i} den_j
+    const uint64_t nb = pk_scan_tmp_elems(n) - 1;
+    const Fr dtot = d2h_fr(st + nb, s);                    // prod of all den_j
+    TRY(pk_mul3(num, den, fe_inv(dtot), key->z_lag.as<Fr>(), n, s));
+    Fr* zc = key->z_coef.as<Fr>();
+    TRY(ntt_run(key->dom, key->z_lag.as<Fr>(), zc, n, -1, 0, nullptr, s, 1));
+    {
+      BlindArgs b{};
+      b.count = 3;
+      for (int i = 0; i < 3; ++i) b.r[i] = rng.fr();
+      TRY(pk_blind(zc, n, b, s));
+    }
+    plk_g1 zcom;
+    TRY(key_commit(key, {zc}, {n + 3}, &zcom, nullptr, s));
+    tr.append_commitment("z", zcom);
+
+    // ---- round 3: quotient (prover.rs:201-287, quotient_poly.rs)
+    const Fr alpha = tr.challenge_scalar("alpha");
+    const Fr range_sep = tr.challenge_scalar("range separation challenge");
+    (void)tr.challenge_scalar("logic separation challenge");
+    (void)tr.challenge_scalar("fixed base separation challenge");
+    (void)tr.challenge_scalar("variable base separation challenge");
+    Fr* pil = key->pi_lag.as<Fr>();
+    PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
+    for (auto& p : pis)
+      PLK_HIP_TRY(hipMemcpyAsync(pil + p.first, &p.second, sizeof(Fr), hipMemcpyHostToDevice, s));
+    TRY(ntt_run(key->dom, pil, key->pi_coef.as<Fr>(), n, -1, 0, nullptr, s, 1));
+    Fr* ev = key->ev8.as<Fr>();  // z, a, b, c, d, pi, l1*alpha^2 over the 8n coset
+    TRY(ntt_run(key->dom8, zc, ev + 0 * n8, n + 3, 1, 1, nullptr, s, 1));
+    for (int c = 0; c < 4; ++c) TRY(ntt_run(key->dom8, wc + c * S, ev + (1 + c) * n8, n + 2, 1, 1, nullptr, s, 1));
+    TRY(ntt_run(key->dom8, key->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nullptr, s, 1));
+    // L1 * alpha^2 = idft(alpha^2 e_0) = alpha^2 / n in every coefficient (quotient_poly.rs:264-272)
+    const Fr alpha2 = fe_sqr(alpha);
+    TRY(pk_fill(key->tmp_a.as<Fr>(), fe_mul(alpha2, key->dom->n_inv), n, s));
+    TRY(ntt_run(key->dom8, key->tmp_a.as<Fr>(), ev + 6 * n8, n, 1, 1, nullptr, s, 1));
+    QuotientArgs qa{};
+    qa.z = ev;
+    qa.a = ev + n8;
+    qa.b = ev + 2 * n8;
+    qa.c = ev + 3 * n8;
+    qa.d = ev + 4 * n8;
+    qa.pi = ev + 5 * n8;
+    qa.l1a = ev + 6 * n8;
+    qa.sel = key->sel8.as<Fr>();
+    qa.sigma = key->sigma8.as<Fr>();
+    qa.elements8 = key->dom8->tw_fwd.as<Fr>();
+    qa.out = key->quot8.as<Fr>();
+    qa.n8 = n8;
+    qa.g = key->dom8->g;
+    qa.alpha = alpha;
+    qa.beta = beta;
+    qa.gamma = gamma;
+    qa.k1 = K1;
+    qa.k2 = K2;
+    qa.k3 = K3;
+    qa.range_sep = range_sep;
+    qa.kappa = fe_sqr(range_sep);
+    qa.kappa2 = fe_sqr(qa.kappa);
+    qa.kappa3 = fe_mul(qa.kappa2, qa.kappa);
+    qa.has_range = key->has_range ? 1 : 0;
+    for (int j = 0; j < 8; ++j) qa.vh_inv[j] = key->vh_inv[j];
+    TRY(pk_quotient(qa, s));
+    Fr* tc = key->t_coef.as<Fr>();
+    TRY(ntt_run(key->dom8, key->quot8.as<Fr>(), tc, n8, -1, 1, nullptr, s, 1));
+    // split into t_low, t_mid, t_high (n each) and t_4 = t[3n..] (prover.rs:252-265)
+    plk_g1 tcom[4];
+    TRY(key_commit(key, {tc, tc + n, tc + 2 * n, tc + 3 * n}, {n, n, n, 5 * n}, tcom, nullptr, s));
+    tr.append_commitment("t_low", tcom[0]);
+    tr.append_commitment("t_mid", tcom[1]);
+    tr.append_commitment("t_high", tcom[2]);
+    tr.append_commitment("t_4", tcom[3]);
+
+    // ---- round 4 / 5: evaluations and linearization (linearization_poly.rs:22-134)
+    const Fr zeta = tr.challenge_scalar("z_challenge");
+    const Fr zw = fe_mul(zeta, key->dom->omega);
+    const Fr* qc = key->q_coef.as<Fr>();
+    const Fr* sc = key->sigma_coef.as<Fr>();
+    EvalBatch eb{};
+    const Fr* polys[16] = {tc, wc, wc + S, wc + 2 * S, wc + 3 * S, sc, sc + n, sc + 2 * n,
+                           qc + QARITH * n, qc + QC * n, qc + QL * n, qc + QR * n,
+                           wc, wc + S, wc + 3 * S, zc};
+    const uint64_t lens[16] = {n8, n + 2, n + 2, n + 2, n + 2, n, n, n, n, n, n, n,
+                               n + 2, n + 2, n + 2, n + 3};
+    for (int i = 0; i < 16; ++i) {
+      eb.poly[i] = polys[i];
+      eb.len[i] = lens[i];
+      eb.x[i] = i < 12 ? zeta : zw;
+    }
+    TRY(pk_eval(eb, 16, n8, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
+    Fr evs[16];
+    PLK_HIP_TRY(hipMemcpyAsync(evs, key->eval_out.ptr, sizeof evs, hipMemcpyDeviceToHost, s));
+    PLK_HIP_TRY(hipStreamSynchronize(s));
+    const Fr t_eval = evs[0], a_e = evs[1], b_e = evs[2], c_e = evs[3], d_e = evs[4];
+    const Fr s1_e = evs[5], s2_e = evs[6], s3_e = evs[7];
+    const Fr qar_e = evs[8], qc_e = evs[9], ql_e = evs[10], qr_e = evs[11];
+    const Fr an_e = evs[12], bn_e = evs[13], dn_e = evs[14], perm_e = evs[15];
+    // r(X) = arithmetic::linearize + range::linearize + permutation::linearize
+    LinComb lc{};
+    auto term = [&](const Fr* p, uint64_t len, const Fr& sc_) {
+      lc.p[lc.terms] = p;
+      lc.len[lc.terms] = len;
+      lc.s[lc.terms] = sc_;
+      ++lc.terms;
+    };
+    term(qc + QM * n, n, fe_mul(qar_e, fe_mul(a_e, b_e)));
+    term(qc + QL * n, n, fe_mul(qar_e, a_e));
+    term(qc + QR * n, n, fe_mul(qar_e, b_e));
+    term(qc + QO * n, n, fe_mul(qar_e, c_e));
+    term(qc + Q4 * n, n, fe_mul(qar_e, d_e));
+    term(qc + QC * n, n, qar_e);
+    if (key->has_range) {
+      const Fr two = fe_dbl(one), three = fe_add(two, one);
+      auto delta = [&](const Fr& f) {
+        return fe_mul(fe_mul(f, fe_sub(f, one)), fe_mul(fe_sub(f, two), fe_sub(f, three)));
+      };
+      auto four = [](const Fr& v) { return fe_dbl(fe_dbl(v)); };
+      Fr r = delta(fe_sub(c_e, four(d_e)));
+      r = fe_add(r, fe_mul(delta(fe_sub(b_e, four(c_e))), qa.kappa));
+      r = fe_add(r, fe_mul(delta(fe_sub(a_e, four(b_e))), qa.kappa2));
+      r = fe_add(r, fe_mul(delta(fe_sub(dn_e, four(a_e))), qa.kappa3));
+      term(qc + QRANGE * n, n, fe_mul(r, range_sep));
+    }
+    (void)an_e;
+    (void)bn_e;
+    // z(X) * [(a + b z + g)(b + b K1 z + g)(c + b K2 z + g)(d + b K3 z + g) alpha + L1(z) alpha^2]
+    const Fr bz = fe_mul(beta, zeta);
+    Fr idc = fe_mul(fe_add(fe_add(a_e, bz), gamma), fe_add(fe_add(b_e, fe_mul(K1, bz)), gamma));
+    idc = fe_mul(idc, fe_add(fe_add(c_e, fe_mul(K2, bz)), gamma));
+    idc = fe_mul(idc, fe_add(fe_add(d_e, fe_mul(K3, bz)), gamma));
+    idc = fe_mul(idc, alpha);
+    const Fr zh = fe_sub(fe_pow_u64(zeta, n), one);  // Z_H(z)
+    const Fr l1 = fe_mul(zh, fe_inv(fe_mul(fr_u64(n), fe_sub(zeta, one))));
+    term(zc, n + 3, fe_add(idc, fe_mul(l1, alpha2)));
+    // -sigma_4(X) * (a + b s1 + g)(b + b s2 + g)(c + b s3 + g) beta perm_eval alpha
+    Fr cpc = fe_add(fe_add(a_e, fe_mul(beta, s1_e)), gamma);
+    cpc = fe_mul(cpc, fe_add(fe_add(b_e, fe_mul(beta, s2_e)), gamma));
+    cpc = fe_mul(cpc, fe_add(fe_add(c_e, fe_mul(beta, s3_e)), gamma));
+    cpc = fe_mul(fe_mul(cpc, fe_mul(beta, perm_e)), alpha);
+    term(sc + 3 * n, n, fe_neg(cpc));
+    Fr* rc = key->r_coef.as<Fr>();
+    TRY(pk_lincomb(lc, rc, n + 3, s));
+    EvalBatch er{};
+    er.poly[0] = rc;
+    er.len[0] = n + 3;
+    er.x[0] = zeta;
+    TRY(pk_eval(er, 1, n8, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
+    const Fr r_e = d2h_fr(key->eval_out.as<Fr>(), s);
+
+    const char* elabels[17] = {"a_eval", "b_eval", "c_eval", "d_eval", "a_next_eval",
+                               "b_next_eval", "d_next_eval", "s_sigma_1_eval", "s_sigma_2_eval",
+                               "s_sigma_3_eval", "q_arith_eval", "q_c_eval", "q_l_eval",
+                               "q_r_eval", "perm_eval", "t_eval", "r_eval"};
+    const Fr evals17[17] = {a_e, b_e, c_e, d_e, an_e, bn_e, dn_e, s1_e, s2_e, s3_e,
+                            qar_e, qc_e, ql_e, qr_e, perm_e, t_eval, r_e};
+    for (int i = 0; i < 17; ++i) tr.append_scalar(elabels[i], evals17[i]);
+
+    // ---- openings (prover.rs:407-452): both v challenges precede both commits
+    const Fr v1 = tr.challenge_scalar("v_challenge");
+    const Fr v2 = tr.challenge_scalar("v_challenge");
+    const Fr zn = fe_pow_u64(zeta, n), z2n = fe_sqr(zn), z3n = fe_mul(z2n, zn);
+    // W(X) = (sum v1^i p_i(X)) / (X - z), p = [quot, r, a, b, c, d, s1, s2, s3]
+    // with quot = t_low + z^n t_mid + z^2n t_high + z^3n t_4 expanded in place
+    LinComb la{};
+    auto lt = [&](const Fr* p, uint64_t len, const Fr& sc_) {
+      la.p[la.terms] = p;
+      la.len[la.terms] = len;
+      la.s[la.terms] = sc_;
+      ++la.terms;
+    };
+    lt(tc, n, one);
+    lt(tc + n, n, zn);
+    lt(tc + 2 * n, n, z2n);
+    lt(tc + 3 * n, 5 * n, z3n);
+    Fr vp = v1;
+    lt(rc, n + 3, vp);
+    for (int c = 0; c < 4; ++c) {
+      vp = fe_mul(vp, v1);
+      lt(wc + c * S, n + 2, vp);
+    }
+    for (int c = 0; c < 3; ++c) {
+      vp = fe_mul(vp, v1);
+      lt(sc + c * n, n, vp);
+    }
+    Fr* ag = key->agg.as<Fr>();
+    TRY(pk_lincomb(la, ag, 5 * n, s));
+    Fr* w1 = key->w_coef.as<Fr>();
+    Fr* w2 = w1 + 5 * n;
+    TRY(pk_ruffini(ag, 5 * n, zeta, w1, key->tmp_a.as<Fr>(), st, s));
+    // W'(X) = (z + v2 a + v2^2 b + v2^3 d) / (X - z w)
+    LinComb lb{};
+    lb.terms = 4;
+    lb.p[0] = zc;
+    lb.len[0] = n + 3;
+    lb.s[0] = one;
+    lb.p[1] = wc;
+    lb.len[1] = n + 2;
+    lb.s[1] = v2;
+    lb.p[2] = wc + S;
+    lb.len[2] = n + 2;
+    lb.s[2] = fe_sqr(v2);
+    lb.p[3] = wc + 3 * S;
+    lb.len[3] = n + 2;
+    lb.s[3] = fe_mul(lb.s[2], v2);
+    Fr* ag2 = key->agg2.as<Fr>();
+    TRY(pk_lincomb(lb, ag2, n + 3, s));
+    TRY(pk_ruffini(ag2, n + 3, zw, w2, key->tmp_a.as<Fr>(), st, s));
+    plk_g1 wcm[2];
+    TRY(key_commit(key, {w1, w2}, {5 * n - 1, n + 2}, wcm, nullptr, s));
+
+    // ---- proof (proof.rs:36-66)
+    proof->a_comm = wcom[0];
+    proof->b_comm = wcom[1];
+    proof->c_comm = wcom[2];
+    proof->d_comm = wcom[3];
+    proof->z_comm = zcom;
+    proof->t_low_comm = tcom[0];
+    proof->t_mid_comm = tcom[1];
+    proof->t_high_comm = tcom[2];
+    proof->t_4_comm = tcom[3];
+    proof->w_z_chall_comm = wcm[0];
+    proof->w_z_chall_w_comm = wcm[1];
+    proof->a_eval = fr_to(a_e);
+    proof->b_eval = fr_to(b_e);
+    proof->c_eval = fr_to(c_e);
+    proof->d_eval = fr_to(d_e);
+    proof->a_next_eval = fr_to(an_e);
+    proof->b_next_eval = fr_to(bn_e);
+    proof->d_next_eval = fr_to(dn_e);
+    proof->q_arith_eval = fr_to(qar_e);
+    proof->q_c_eval = fr_to(qc_e);
+    proof->q_l_eval = fr_to(ql_e);
+    proof->q_r_eval = fr_to(qr_e);
+    proof->s_sigma_1_eval = fr_to(s1_e);
+    proof->s_sigma_2_eval = fr_to(s2_e);
+    proof->s_sigma_3_eval = fr_to(s3_e);
+    proof->r_poly_eval = fr_to(r_e);
+    proof->perm_eval = fr_to(perm_e);
+    return PLK_OK;
+  } catch (const std::bad_alloc&) {
+    return PLK_E_OOM;
+  } catch (...) {
+    return PLK_E_DEVICE;
+  }
+}
+
+}  // extern "C"

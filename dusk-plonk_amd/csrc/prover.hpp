@@ -1,0 +1,107 @@
+// prover.hpp — composer, proving key and prover objects behind the plk_composer / plk_key /
+// plk_prove entry points of include/plk.h, and the kernel-argument structs of
+// prover_kernels.hip.
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace plk {
+
+// ---- kernel arguments --------------------------------------------------------------
+struct BlindArgs {
+  Fr r[4];
+  uint32_t count;
+};
+
+// selector rows of the 8n evaluation table
+enum { SEL_QM = 0, SEL_QL, SEL_QR, SEL_QO, SEL_Q4, SEL_QC, SEL_QARITH, SEL_QRANGE, SEL_COUNT8 };
+
+struct QuotientArgs {
+  const Fr *a, *b, *c, *d, *z, *pi, *l1a, *sel, *sigma, *elements8;
+  Fr* out;
+  uint64_t n8;
+  Fr g, alpha, beta, gamma, k1, k2, k3;
+  Fr range_sep, kappa, kappa2, kappa3;
+  int has_range;
+  Fr vh_inv[8];
+};
+
+constexpr int kMaxEval = 16;
+struct EvalBatch {
+  const Fr* poly[kMaxEval];
+  uint64_t len[kMaxEval];
+  Fr x[kMaxEval];
+};
+
+constexpr int kMaxTerms = 12;
+struct LinComb {
+  const Fr* p[kMaxTerms];
+  uint64_t len[kMaxTerms];
+  Fr s[kMaxTerms];
+  uint32_t terms;
+};
+
+int pk_gather_wires(const Fr* witness, const uint32_t* idx, uint64_t m, uint64_t n, Fr* out,
+                    hipStream_t s);
+int pk_blind(Fr* poly, uint64_t n, const BlindArgs& b, hipStream_t s);
+int pk_fill(Fr* out, const Fr& v, uint64_t n, hipStream_t s);
+int pk_perm_numden(const Fr* wires, const Fr* sigmas, const Fr* elements, uint64_t n,
+                   const Fr& beta, const Fr& gamma, const Fr& k1, const Fr& k2, const Fr& k3,
+                   Fr* num, Fr* den, hipStream_t s);
+int pk_mul3(const Fr* a, const Fr* b, const Fr& c, Fr* out, uint64_t n, hipStream_t s);
+uint64_t pk_scan_tmp_elems(uint64_t n);
+int pk_scan(const Fr* in, Fr* out, uint64_t n, bool mul, bool suffix, bool exclusive, Fr* tmp,
+            hipStream_t s);
+int pk_quotient(const QuotientArgs& q, hipStream_t s);
+uint32_t pk_eval_max_blocks(uint64_t max_len);
+int pk_eval(const EvalBatch& e, uint32_t count, uint64_t max_len, Fr* partial, Fr* d_out,
+            hipStream_t s);
+int pk_lincomb(const LinComb& lc, Fr* out, uint64_t len_out, hipStream_t s);
+int pk_scale_powers(const Fr* c, uint64_t len, const Fr& x, uint64_t shift, Fr* y, hipStream_t s);
+int pk_ruffini(const Fr* c, uint64_t len, const Fr& z, Fr* q, Fr* tmp, Fr* scan_tmp,
+               hipStream_t s);
+
+// ---- composer (host) ---------------------------------------------------------------
+// One width-4 gate: q_m a b + q_l a + q_r b + q_o o + q_4 d + q_c + PI = 0 (lib.rs:546)
+struct Gate {
+  Fr q[11];  // q_m q_l q_r q_o q_4 q_c q_arith q_range q_logic q_fixed_group_add q_variable_group_add
+  uint32_t w[4];  // a, b, o, d witness indices
+  bool has_pi;
+  Fr pi;
+};
+
+}  // namespace plk
+
+struct plk_composer {
+  std::vector<plk::Fr> witness;
+  std::vector<plk::Gate> gates;
+  // witness -> wires in insertion order (permutation.rs:21-25,72-104): wire = 4*gate + col
+  std::vector<std::vector<uint32_t>> wire_map;
+};
+
+struct plk_key {
+  plk_ctx* ctx = nullptr;
+  plk_srs* srs = nullptr;
+  std::string label;
+  uint64_t m = 0, n = 0, n_trim = 0;
+  uint32_t k = 0;
+  plk_domain* dom = nullptr;   // n
+  plk_domain* dom8 = nullptr;  // 8n
+  bool has_range = false;
+  std::vector<plk::Gate> gates;  // structure the key was compiled from (selectors, wiring)
+  // device-resident proving key
+  plk::DevBuf q_coef;       // 11 x n selector coefficient polys
+  plk::DevBuf sel8;         // SEL_COUNT8 x 8n coset evaluations
+  plk::DevBuf sigma_coef;   // 4 x n
+  plk::DevBuf sigma_lag;    // 4 x n Lagrange values (= dft of sigma_coef, cached)
+  plk::DevBuf sigma8;       // 4 x 8n
+  plk::DevBuf wire_idx;     // 4 x n witness indices per gate (u32)
+  plk::Fr vh_inv[8];
+  plk_g1 comms[15];         // q_m q_l q_r q_o q_c q_4 q_arith q_range q_logic q_fixed q_var s1..s4
+  // per-proof scratch
+  plk::DevBuf witness, wires_lag, wires_coef, z_lag, z_coef, num, den, tmp_a, tmp_b, scan_tmp,
+      pi_lag, pi_coef, ev8, quot8, t_coef, r_coef, agg, agg2, w_coef, eval_partial, eval_out;
+};

@@ -1,0 +1,421 @@
+// prover_kernels.hip — device kernels of Prover::create_proof around the NTT/MSM path
+// (SURVEY.md §8f rows 1-3 and §8a a9/a12), all HBM- or VALU-bound elementwise work:
+//  * wire gather (prover.rs:109-119), blinding b(X)(X^n - 1) (prover.rs:126-129,193)
+//  * grand product z (permutation.rs:205-300): per-gate numerator/denominator, then
+//    z_i = N_i * S_i / D (exclusive prefix product of numerators, inclusive suffix product
+//    of denominators, ONE inversion) instead of the reference's n inversions + serial scan
+//  * quotient over the 8n coset (quotient_poly.rs:74-114,122-262): arithmetic + range
+//    widgets + PI + permutation identity/copy terms + L1 term, divided by v_h, whose
+//    8 distinct values (period 8) are inverted once on the host
+//  * batched polynomial evaluation (linearization_poly.rs:52-73,108)
+//  * linear combinations (t split / quot assembly prover.rs:252-259,408-418, r(X),
+//    aggregate witness numerators) and Ruffini division by (X - z)
+#include <hip/hip_runtime.h>
+
+#include "internal.hpp"
+#include "prover.hpp"
+
+namespace plk {
+
+namespace {
+
+__device__ __forceinline__ Fr ldf(const Fr* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  Fr r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+
+__device__ __forceinline__ void stf(Fr* p, const Fr& v) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+  q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+}
+
+inline uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
+
+// ---------------------------------------------------------------------------- wires
+__global__ void k_gather_wires(const Fr* __restrict__ witness, const uint32_t* __restrict__ idx,
+                               uint64_t m, uint64_t n, Fr* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t col = blockIdx.y;
+  if (i >= n) return;
+  stf(&out[col * n + i], i < m ? ldf(&witness[idx[col * n + i]]) : fe_zero<FrCfg>());
+}
+
+// poly[i] -= r_i, poly[n + i] = r_i (i < count): p(X) + b(X)(X^n - 1)
+__global__ void k_blind(Fr* __restrict__ poly, uint64_t n, BlindArgs b) {
+  const uint32_t i = threadIdx.x;
+  if (i >= b.count) return;
+  stf(&poly[i], fe_sub(ldf(&poly[i]), b.r[i]));
+  stf(&poly[n + i], b.r[i]);
+}
+
+__global__ void k_fill(Fr* __restrict__ out, Fr v, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) stf(&out[i], v);
+}
+
+// ------------------------------------------------------------------- grand product
+// num_i = prod_c (w_c + beta k_c w^i + gamma), den_i = prod_c (w_c + beta sigma_c + gamma)
+__global__ void k_perm_numden(const Fr* __restrict__ wires, const Fr* __restrict__ sigmas,
+                              const Fr* __restrict__ elements, uint64_t n, Fr beta, Fr gamma,
+                              Fr k1, Fr k2, Fr k3, Fr* __restrict__ num, Fr* __restrict__ den) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr x = ldf(&elements[i]);
+  const Fr bx = fe_mul(beta, x);
+  const Fr ks[4] = {fe_one<FrCfg>(), k1, k2, k3};
+  Fr nu = fe_one<FrCfg>(), de = fe_one<FrCfg>();
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const Fr w = ldf(&wires[c * n + i]);
+    const Fr wg = fe_add(w, gamma);
+    nu = fe_mul(nu, fe_add(wg, c == 0 ? bx : fe_mul(ks[c], bx)));
+    de = fe_mul(de, fe_add(wg, fe_mul(beta, ldf(&sigmas[c * n + i]))));
+  }
+  stf(&num[i], nu);
+  stf(&den[i], de);
+}
+
+// z_i = N_i * S_i * dinv
+__global__ void k_mul3(const Fr* __restrict__ a, const Fr* __restrict__ b, Fr c,
+                       Fr* __restrict__ out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) stf(&out[i], fe_mul(fe_mul(ldf(&a[i]), ldf(&b[i])), c));
+}
+
+// ----------------------------------------------------------------------- scans
+// 3-phase scan over Fr with op = multiply (MUL) or add; SUFFIX scans from the top.
+constexpr uint32_t kScanThreads = 256, kScanPer = 8, kScanBlock = kScanThreads * kScanPer;
+
+template <bool MUL>
+__device__ __forceinline__ Fr op(const Fr& a, const Fr& b) {
+  return MUL ? fe_mul(a, b) : fe_add(a, b);
+}
+template <bool MUL>
+__device__ __forceinline__ Fr ident() {
+  return MUL ? fe_one<FrCfg>() : fe_zero<FrCfg>();
+}
+
+// logical index j of a scan in direction SUFFIX maps to physical n-1-j
+template <bool SUFFIX>
+__device__ __forceinline__ uint64_t phys(uint64_t j, uint64_t n) {
+  return SUFFIX ? n - 1 - j : j;
+}
+
+template <bool MUL, bool SUFFIX>
+__global__ void __launch_bounds__(kScanThreads) k_scan_reduce(const Fr* __restrict__ in, uint64_t n,
+                                                              Fr* __restrict__ tot) {
+  __shared__ Fr sh[kScanThreads];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+  Fr acc = ident<MUL>();
+  for (uint32_t k = 0; k < kScanPer; ++k)
+    if (base + k < n) acc = op<MUL>(acc, ldf(&in[phys<SUFFIX>(base + k, n)]));
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t h = kScanThreads / 2; h >= 1; h >>= 1) {
+    if (threadIdx.x < h) sh[threadIdx.x] = op<MUL>(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) stf(&tot[blockIdx.x], sh[0]);
+}
+
+// exclusive scan of the block totals in place (single workgroup); tot[nb] = grand total
+template <bool MUL>
+__global__ void __launch_bounds__(kScanThreads) k_scan_tops(Fr* __restrict__ tot, uint32_t nb) {
+  __shared__ Fr sh[kScanThreads];
+  const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
+  const uint32_t b0 = threadIdx.x * per;
+  Fr acc = ident<MUL>();
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) acc = op<MUL>(acc, ldf(&tot[b]));
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t off = 1; off < kScanThreads; off <<= 1) {
+    Fr v = threadIdx.x >= off ? sh[threadIdx.x - off] : ident<MUL>();
+    __syncthreads();
+    sh[threadIdx.x] = op<MUL>(sh[threadIdx.x], v);
+    __syncthreads();
+  }
+  Fr run = threadIdx.x ? sh[threadIdx.x - 1] : ident<MUL>();
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
+    const Fr v = ldf(&tot[b]);
+    stf(&tot[b], run);
+    run = op<MUL>(run, v);
+  }
+  if (threadIdx.x == kScanThreads - 1) stf(&tot[nb], sh[kScanThreads - 1]);
+}
+
+template <bool MUL, bool SUFFIX, bool EXCL>
+__global__ void __launch_bounds__(kScanThreads) k_scan_apply(const Fr* __restrict__ in, uint64_t n,
+                                                             const Fr* __restrict__ tot,
+                                                             Fr* __restrict__ out) {
+  __shared__ Fr sh[kScanThreads];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+  Fr acc = ident<MUL>();
+  for (uint32_t k = 0; k < kScanPer; ++k)
+    if (base + k < n) acc = op<MUL>(acc, ldf(&in[phys<SUFFIX>(base + k, n)]));
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t off = 1; off < kScanThreads; off <<= 1) {
+    Fr v = threadIdx.x >= off ? sh[threadIdx.x - off] : ident<MUL>();
+    __syncthreads();
+    sh[threadIdx.x] = op<MUL>(sh[threadIdx.x], v);
+    __syncthreads();
+  }
+  Fr run = op<MUL>(ldf(&tot[blockIdx.x]), threadIdx.x ? sh[threadIdx.x - 1] : ident<MUL>());
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    if (base + k >= n) break;
+    const uint64_t p = phys<SUFFIX>(base + k, n);
+    const Fr v = ldf(&in[p]);
+    if (EXCL) {
+      stf(&out[p], run);
+      run = op<MUL>(run, v);
+    } else {
+      run = op<MUL>(run, v);
+      stf(&out[p], run);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------ quotient
+__global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t N = q.n8;
+  if (i >= N) return;
+  const uint64_t nx = (i + 8) & (N - 1);  // "next row" of the n-domain inside the 8n domain
+  const Fr a = ldf(&q.a[i]), b = ldf(&q.b[i]), c = ldf(&q.c[i]), d = ldf(&q.d[i]);
+  const Fr z = ldf(&q.z[i]), z_next = ldf(&q.z[nx]);
+  // arithmetic widget: q_arith (q_m a b + q_l a + q_r b + q_o c + q_4 d + q_c)
+  Fr t = fe_mul(ldf(&q.sel[SEL_QM * N + i]), fe_mul(a, b));
+  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_QL * N + i]), a));
+  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_QR * N + i]), b));
+  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_QO * N + i]), c));
+  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_Q4 * N + i]), d));
+  t = fe_add(t, ldf(&q.sel[SEL_QC * N + i]));
+  t = fe_mul(t, ldf(&q.sel[SEL_QARITH * N + i]));
+  t = fe_add(t, ldf(&q.pi[i]));
+  // range widget: sep * q_range * (D(c-4d) + D(b-4c) k + D(a-4b) k^2 + D(d_next-4a) k^3)
+  if (q.has_range) {
+    const Fr qr = ldf(&q.sel[SEL_QRANGE * N + i]);
+    if (!fe_is_zero(qr)) {
+      const Fr d_next = ldf(&q.d[nx]);
+      const Fr one = fe_one<FrCfg>();
+      const Fr two = fe_dbl(one), three = fe_add(two, one);
+      auto delta = [&](const Fr& f) {
+        return fe_mul(fe_mul(f, fe_sub(f, one)), fe_mul(fe_sub(f, two), fe_sub(f, three)));
+      };
+      auto four = [](const Fr& x) { return fe_dbl(fe_dbl(x)); };
+      Fr r = delta(fe_sub(c, four(d)));
+      r = fe_add(r, fe_mul(delta(fe_sub(b, four(c))), q.kappa));
+      r = fe_add(r, fe_mul(delta(fe_sub(a, four(b))), q.kappa2));
+      r = fe_add(r, fe_mul(delta(fe_sub(d_next, four(a))), q.kappa3));
+      t = fe_add(t, fe_mul(fe_mul(r, qr), q.range_sep));
+    }
+  }
+  // permutation: alpha [ z (a + bX + g)(b + bK1X + g)(c + bK2X + g)(d + bK3X + g)
+  //                    - z_next (a + b s1 + g)(b + b s2 + g)(c + b s3 + g)(d + b s4 + g) ]
+  //              + (z - 1) L1(X) alpha^2
+  const Fr X = fe_mul(q.g, ldf(&q.elements8[i]));
+  const Fr bX = fe_mul(q.beta, X);
+  Fr id = fe_mul(fe_add(fe_add(a, bX), q.gamma), fe_add(fe_add(b, fe_mul(q.k1, bX)), q.gamma));
+  id = fe_mul(id, fe_add(fe_add(c, fe_mul(q.k2, bX)), q.gamma));
+  id = fe_mul(id, fe_add(fe_add(d, fe_mul(q.k3, bX)), q.gamma));
+  id = fe_mul(id, z);
+  Fr cp = fe_add(fe_add(a, fe_mul(q.beta, ldf(&q.sigma[0 * N + i]))), q.gamma);
+  cp = fe_mul(cp, fe_add(fe_add(b, fe_mul(q.beta, ldf(&q.sigma[1 * N + i]))), q.gamma));
+  cp = fe_mul(cp, fe_add(fe_add(c, fe_mul(q.beta, ldf(&q.sigma[2 * N + i]))), q.gamma));
+  cp = fe_mul(cp, fe_add(fe_add(d, fe_mul(q.beta, ldf(&q.sigma[3 * N + i]))), q.gamma));
+  cp = fe_mul(cp, z_next);
+  Fr perm = fe_mul(fe_sub(id, cp), q.alpha);
+  perm = fe_add(perm, fe_mul(fe_sub(z, fe_one<FrCfg>()), ldf(&q.l1a[i])));
+  stf(&q.out[i], fe_mul(fe_add(t, perm), q.vh_inv[i & 7]));
+}
+
+// -------------------------------------------------------------------- evaluation
+constexpr uint32_t kEvalThreads = 256, kEvalPer = 16, kEvalBlock = kEvalThreads * kEvalPer;
+
+// partial[k][blk] = sum_{j in block} c_j x^j   (poly k of the batch)
+__global__ void __launch_bounds__(kEvalThreads) k_eval_partial(EvalBatch e, Fr* __restrict__ partial,
+                                                               uint32_t max_blocks) {
+  __shared__ Fr sh[kEvalThreads];
+  const uint32_t k = blockIdx.y;
+  const Fr* p = e.poly[k];
+  const uint64_t len = e.len[k];
+  const Fr x = e.x[k];
+  const uint64_t base = (uint64_t)blockIdx.x * kEvalBlock + (uint64_t)threadIdx.x * kEvalPer;
+  Fr acc = fe_zero<FrCfg>();
+  if (base < len) {
+    // Horner over this thread's run, then scale by x^base
+    const uint64_t top = base + kEvalPer < len ? base + kEvalPer : len;
+    for (uint64_t j = top; j-- > base;) acc = fe_add(fe_mul(acc, x), ldf(&p[j]));
+    acc = fe_mul(acc, fe_pow_u64(x, base));
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t h = kEvalThreads / 2; h >= 1; h >>= 1) {
+    if (threadIdx.x < h) sh[threadIdx.x] = fe_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) stf(&partial[(size_t)k * max_blocks + blockIdx.x], sh[0]);
+}
+
+__global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restrict__ partial,
+                                                             uint32_t nblocks, uint32_t max_blocks,
+                                                             Fr* __restrict__ out) {
+  __shared__ Fr sh[kEvalThreads];
+  const uint32_t k = blockIdx.x;
+  Fr acc = fe_zero<FrCfg>();
+  for (uint32_t b = threadIdx.x; b < nblocks; b += kEvalThreads)
+    acc = fe_add(acc, ldf(&partial[(size_t)k * max_blocks + b]));
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t h = kEvalThreads / 2; h >= 1; h >>= 1) {
+    if (threadIdx.x < h) sh[threadIdx.x] = fe_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) stf(&out[k], sh[0]);
+}
+
+// ---------------------------------------------------------------- linear combos
+// out[j] = sum_t s_t * p_t[j] (p_t[j] = 0 past len_t), j < len_out
+__global__ void k_lincomb(LinComb lc, Fr* __restrict__ out, uint64_t len_out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= len_out) return;
+  Fr acc = fe_zero<FrCfg>();
+  for (uint32_t t = 0; t < lc.terms; ++t)
+    if (j < lc.len[t]) acc = fe_add(acc, fe_mul(lc.s[t], ldf(&lc.p[t][j])));
+  stf(&out[j], acc);
+}
+
+// y_j = c_j * x^j (per-thread run of 16: one pow, then successive multiplies)
+__global__ void k_scale_powers(const Fr* __restrict__ c, uint64_t len, Fr x, uint64_t shift,
+                               Fr* __restrict__ y) {
+  const uint64_t j0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (j0 >= len) return;
+  Fr p = fe_pow_u64(x, j0 + shift);
+  const uint64_t j1 = j0 + 16 < len ? j0 + 16 : len;
+  for (uint64_t j = j0; j < j1; ++j) {
+    stf(&y[j], fe_mul(ldf(&c[j]), p));
+    p = fe_mul(p, x);
+  }
+}
+
+}  // namespace
+
+// ============================================================== host launchers
+int pk_gather_wires(const Fr* witness, const uint32_t* idx, uint64_t m, uint64_t n, Fr* out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_wires, dim3(blocks_for(n, 256), 4), dim3(256), 0, s, witness, idx, m,
+                     n, out);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_blind(Fr* poly, uint64_t n, const BlindArgs& b, hipStream_t s) {
+  hipLaunchKernelGGL(k_blind, dim3(1), dim3(64), 0, s, poly, n, b);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_fill(Fr* out, const Fr& v, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(blocks_for(n, 256)), dim3(256), 0, s, out, v, n);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_perm_numden(const Fr* wires, const Fr* sigmas, const Fr* elements, uint64_t n,
+                   const Fr& beta, const Fr& gamma, const Fr& k1, const Fr& k2, const Fr& k3,
+                   Fr* num, Fr* den, hipStream_t s) {
+  hipLaunchKernelGGL(k_perm_numden, dim3(blocks_for(n, 256)), dim3(256), 0, s, wires, sigmas,
+                     elements, n, beta, gamma, k1, k2, k3, num, den);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_mul3(const Fr* a, const Fr* b, const Fr& c, Fr* out, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_mul3, dim3(blocks_for(n, 256)), dim3(256), 0, s, a, b, c, out, n);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+uint64_t pk_scan_tmp_elems(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock + 1; }
+
+int pk_scan(const Fr* in, Fr* out, uint64_t n, bool mul, bool suffix, bool exclusive, Fr* tmp,
+            hipStream_t s) {
+  if (n == 0) return PLK_OK;
+  const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+#define SCAN3(M, S, E)                                                                         \
+  do {                                                                                         \
+    hipLaunchKernelGGL((k_scan_reduce<M, S>), dim3(nb), dim3(kScanThreads), 0, s, in, n, tmp); \
+    hipLaunchKernelGGL((k_scan_tops<M>), dim3(1), dim3(kScanThreads), 0, s, tmp, nb);          \
+    hipLaunchKernelGGL((k_scan_apply<M, S, E>), dim3(nb), dim3(kScanThreads), 0, s, in, n, tmp, \
+                       out);                                                                   \
+  } while (0)
+  if (mul) {
+    if (suffix) {
+      if (exclusive) SCAN3(true, true, true); else SCAN3(true, true, false);
+    } else {
+      if (exclusive) SCAN3(true, false, true); else SCAN3(true, false, false);
+    }
+  } else {
+    if (suffix) {
+      if (exclusive) SCAN3(false, true, true); else SCAN3(false, true, false);
+    } else {
+      if (exclusive) SCAN3(false, false, true); else SCAN3(false, false, false);
+    }
+  }
+#undef SCAN3
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_quotient(const QuotientArgs& q, hipStream_t s) {
+  hipLaunchKernelGGL(k_quotient, dim3(blocks_for(q.n8, 256)), dim3(256), 0, s, q);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+uint32_t pk_eval_max_blocks(uint64_t max_len) {
+  return (uint32_t)((max_len + kEvalBlock - 1) / kEvalBlock);
+}
+
+int pk_eval(const EvalBatch& e, uint32_t count, uint64_t max_len, Fr* partial, Fr* d_out,
+            hipStream_t s) {
+  const uint32_t mb = pk_eval_max_blocks(max_len ? max_len : 1);
+  hipLaunchKernelGGL(k_eval_partial, dim3(mb, count), dim3(kEvalThreads), 0, s, e, partial, mb);
+  hipLaunchKernelGGL(k_eval_final, dim3(count), dim3(kEvalThreads), 0, s, partial, mb, mb, d_out);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_lincomb(const LinComb& lc, Fr* out, uint64_t len_out, hipStream_t s) {
+  if (len_out == 0) return PLK_OK;
+  hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(len_out, 256)), dim3(256), 0, s, lc, out, len_out);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_scale_powers(const Fr* c, uint64_t len, const Fr& x, uint64_t shift, Fr* y, hipStream_t s) {
+  if (len == 0) return PLK_OK;
+  hipLaunchKernelGGL(k_scale_powers, dim3(blocks_for((len + 15) / 16, 256)), dim3(256), 0, s, c, len,
+                     x, shift, y);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+// Ruffini: q(X) = (p(X) - p(z)) / (X - z), q_k = z^-(k+1) * sum_{j>k} c_j z^j, len(q) = len - 1.
+// tmp holds len elements + scan tmp.
+int pk_ruffini(const Fr* c, uint64_t len, const Fr& z, Fr* q, Fr* tmp, Fr* scan_tmp,
+               hipStream_t s) {
+  if (len <= 1) return PLK_OK;
+  int st;
+  if ((st = pk_scale_powers(c, len, z, 0, tmp, s))) return st;          // y_j = c_j z^j
+  if ((st = pk_scan(tmp, tmp, len, false, true, true, scan_tmp, s))) return st;  // S_j = sum_{i>j} y_i
+  const Fr zinv = fe_inv(z);
+  return pk_scale_powers(tmp, len - 1, zinv, 1, q, s);                  // q_k = S_k z^-(k+1)
+}
+
+}  // namespace plk

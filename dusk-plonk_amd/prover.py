@@ -1,0 +1,308 @@
+"""Host-side mirror of the reference's prover API over the C ABI (include/plk.h):
+
+* ``Constraint`` — zksnarks::Constraint builder (``mult/left/right/output/fourth/constant/
+  public/a/b/o/d``), values as Python ints (canonical Fr) or Montgomery limb arrays.
+* ``Plonk`` — the composer (``src/lib.rs``: ``append_witness``, ``append_public``,
+  ``append_gate``, ``gate_add``, ``gate_mul``, ``assert_equal``, ``assert_equal_constant``,
+  ``component_boolean``); ``Plonk()`` is ``Plonk::initialize()``.
+* ``PlonkKey.compile_with_circuit(pp, label, circuit)`` — ``src/key.rs:63-327``, returning
+  ``(Prover, VerifierData)``; ``Prover.create_proof(seed, circuit)`` — ``src/prover.rs:67``,
+  returning ``(Proof, public_inputs)``. A circuit is any object with
+  ``synthesize(composer)`` (the reference's ``Circuit`` trait).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .plonk import (PLK_OK, PlonkError, PlonkParams, _check, _lib, _ptr)
+
+R_MOD = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+_R = 1 << 256
+
+
+class PlkFr(C.Structure):
+    _fields_ = [("l", C.c_uint64 * 4)]
+
+
+class PlkG1(C.Structure):
+    _fields_ = [("x", C.c_uint64 * 6), ("y", C.c_uint64 * 6), ("infinity", C.c_uint64)]
+
+
+_SEL = ["q_m", "q_l", "q_r", "q_o", "q_4", "q_c", "q_arith", "q_range", "q_logic",
+        "q_fixed_group_add", "q_variable_group_add"]
+
+
+class PlkConstraint(C.Structure):
+    _fields_ = [(s, PlkFr) for s in _SEL] + [
+        ("a", C.c_uint32), ("b", C.c_uint32), ("o", C.c_uint32), ("d", C.c_uint32),
+        ("has_public", C.c_uint32), ("_pad", C.c_uint32), ("public_input", PlkFr)]
+
+
+_COMMS = ["a_comm", "b_comm", "c_comm", "d_comm", "z_comm", "t_low_comm", "t_mid_comm",
+          "t_high_comm", "t_4_comm", "w_z_chall_comm", "w_z_chall_w_comm"]
+_EVALS = ["a_eval", "b_eval", "c_eval", "d_eval", "a_next_eval", "b_next_eval", "d_next_eval",
+          "q_arith_eval", "q_c_eval", "q_l_eval", "q_r_eval", "s_sigma_1_eval",
+          "s_sigma_2_eval", "s_sigma_3_eval", "r_poly_eval", "perm_eval"]
+
+
+class PlkProof(C.Structure):
+    _fields_ = [(c, PlkG1) for c in _COMMS] + [(e, PlkFr) for e in _EVALS]
+
+
+def _bind():
+    lib = _lib()
+    if getattr(lib, "_prover_bound", False):
+        return lib
+    vp, u32, u64, sz, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_size_t, C.c_int
+    pp = C.POINTER(C.c_void_p)
+    sig = {
+        "plk_composer_create": [pp], "plk_composer_destroy": [vp],
+        "plk_composer_size": [vp, C.POINTER(sz), C.POINTER(sz)],
+        "plk_composer_append_witness": [vp, vp, C.POINTER(u32)],
+        "plk_composer_witness_value": [vp, u32, vp],
+        "plk_composer_set_witness": [vp, u32, vp],
+        "plk_composer_append_public": [vp, vp, C.POINTER(u32)],
+        "plk_composer_append_gate": [vp, vp], "plk_composer_append_custom_gate": [vp, vp],
+        "plk_composer_gate_eval": [vp, vp, C.POINTER(u32)],
+        "plk_composer_assert_equal": [vp, u32, u32],
+        "plk_composer_assert_equal_constant": [vp, u32, vp, vp],
+        "plk_composer_component_boolean": [vp, u32],
+        "plk_composer_synthetic_chain": [vp, sz, u64],
+        "plk_composer_public_inputs": [vp, vp, vp, sz, C.POINTER(sz)],
+        "plk_key_compile": [vp, vp, C.c_char_p, pp], "plk_key_destroy": [vp],
+        "plk_key_info": [vp, C.POINTER(u64), C.POINTER(u64), vp],
+        "plk_prove": [vp, vp, u64, vp, vp, sz, C.POINTER(sz)],
+    }
+    for name, args in sig.items():
+        f = getattr(lib, name)
+        f.restype, f.argtypes = i32, args
+    lib._prover_bound = True
+    return lib
+
+
+def _fr(v) -> PlkFr:
+    """Python int (canonical) or Montgomery limb array -> PlkFr (Montgomery)."""
+    out = PlkFr()
+    if isinstance(v, (int, np.integer)):
+        m = (int(v) % R_MOD) * _R % R_MOD
+        for i in range(4):
+            out.l[i] = (m >> (64 * i)) & 0xFFFFFFFFFFFFFFFF
+    else:
+        a = np.asarray(v, dtype=np.uint64).reshape(4)
+        for i in range(4):
+            out.l[i] = int(a[i])
+    return out
+
+
+def fr_limbs(p: PlkFr) -> np.ndarray:
+    return np.array([p.l[i] for i in range(4)], dtype=np.uint64)
+
+
+def fr_int(p) -> int:
+    """Montgomery limbs (PlkFr or array) -> canonical int."""
+    a = fr_limbs(p) if isinstance(p, PlkFr) else np.asarray(p, dtype=np.uint64)
+    v = sum(int(a[i]) << (64 * i) for i in range(4))
+    return v * pow(_R, -1, R_MOD) % R_MOD
+
+
+class Constraint:
+    """zksnarks::Constraint builder (selectors default 0, wires default Plonk::ZERO)."""
+
+    def __init__(self):
+        self.c = PlkConstraint()
+
+    def _set(self, name, v):
+        setattr(self.c, name, _fr(v))
+        return self
+
+    def mult(self, v):
+        return self._set("q_m", v)
+
+    def left(self, v):
+        return self._set("q_l", v)
+
+    def right(self, v):
+        return self._set("q_r", v)
+
+    def output(self, v):
+        return self._set("q_o", v)
+
+    def fourth(self, v):
+        return self._set("q_4", v)
+
+    def constant(self, v):
+        return self._set("q_c", v)
+
+    def range(self, v):
+        return self._set("q_range", v)
+
+    def public(self, v):
+        self.c.has_public = 1
+        self.c.public_input = _fr(v)
+        return self
+
+    def a(self, w):
+        self.c.a = w
+        return self
+
+    def b(self, w):
+        self.c.b = w
+        return self
+
+    def o(self, w):
+        self.c.o = w
+        return self
+
+    def d(self, w):
+        self.c.d = w
+        return self
+
+
+class Plonk:
+    """The composer, Plonk<JubjubAffine> (src/lib.rs:103-115); construction = initialize()."""
+
+    ZERO = 0
+    ONE = 1
+
+    def __init__(self):
+        lib = _bind()
+        h = C.c_void_p()
+        _check(lib.plk_composer_create(C.byref(h)), "plk_composer_create")
+        self._h = h
+
+    def __del__(self):
+        try:
+            if self._h:
+                _bind().plk_composer_destroy(self._h)
+        except Exception:
+            pass
+
+    def m(self) -> int:
+        g = C.c_size_t()
+        _check(_bind().plk_composer_size(self._h, C.byref(g), None), "size")
+        return g.value
+
+    def append_witness(self, v) -> int:
+        w = C.c_uint32()
+        f = _fr(v)
+        _check(_bind().plk_composer_append_witness(self._h, C.byref(f), C.byref(w)), "witness")
+        return w.value
+
+    def __getitem__(self, w) -> int:
+        f = PlkFr()
+        _check(_bind().plk_composer_witness_value(self._h, w, C.byref(f)), "witness_value")
+        return fr_int(f)
+
+    def append_public(self, v) -> int:
+        w = C.c_uint32()
+        f = _fr(v)
+        _check(_bind().plk_composer_append_public(self._h, C.byref(f), C.byref(w)), "public")
+        return w.value
+
+    def append_gate(self, c: Constraint):
+        _check(_bind().plk_composer_append_gate(self._h, C.byref(c.c)), "append_gate")
+
+    def append_custom_gate(self, c: Constraint):
+        _check(_bind().plk_composer_append_custom_gate(self._h, C.byref(c.c)), "custom_gate")
+
+    def gate_add(self, c: Constraint) -> int:
+        w = C.c_uint32()
+        _check(_bind().plk_composer_gate_eval(self._h, C.byref(c.c), C.byref(w)), "gate_add")
+        return w.value
+
+    gate_mul = gate_add  # both evaluate o with q_o = -1 (lib.rs:1169-1197)
+
+    def assert_equal(self, a: int, b: int):
+        _check(_bind().plk_composer_assert_equal(self._h, a, b), "assert_equal")
+
+    def assert_equal_constant(self, a: int, constant, public=None):
+        c = _fr(constant)
+        p = None if public is None else C.byref(_fr(public))
+        _check(_bind().plk_composer_assert_equal_constant(self._h, a, C.byref(c), p),
+               "assert_equal_constant")
+
+    def component_boolean(self, a: int):
+        _check(_bind().plk_composer_component_boolean(self._h, a), "component_boolean")
+
+    def synthetic_chain(self, gates: int, seed: int):
+        _check(_bind().plk_composer_synthetic_chain(self._h, gates, seed), "synthetic_chain")
+
+    def public_inputs(self):
+        cnt = C.c_size_t()
+        lib = _bind()
+        _check(lib.plk_composer_public_inputs(self._h, None, None, 0, C.byref(cnt)), "pi")
+        vals = (PlkFr * max(1, cnt.value))()
+        idx = (C.c_uint64 * max(1, cnt.value))()
+        _check(lib.plk_composer_public_inputs(self._h, vals, idx, cnt.value, C.byref(cnt)), "pi")
+        return [fr_int(vals[i]) for i in range(cnt.value)], [idx[i] for i in range(cnt.value)]
+
+
+class Proof:
+    """zksnarks Proof: 11 commitments (uint64[13] each) and 16 evaluations (canonical ints)."""
+
+    def __init__(self, raw: PlkProof):
+        self.raw = raw
+        for c in _COMMS:
+            g = getattr(raw, c)
+            setattr(self, c, np.array(list(g.x) + list(g.y) + [g.infinity], dtype=np.uint64))
+        for e in _EVALS:
+            setattr(self, e, fr_int(getattr(raw, e)))
+
+    def to_bytes(self) -> bytes:
+        return bytes(self.raw)
+
+
+class VerifierData:
+    """What Verifier::new receives (verifier.rs:24-44): label, m, the 15 commitments in
+    transcript order, public input indexes."""
+
+    def __init__(self, label: bytes, n: int, m: int, comms: np.ndarray, pi_indexes):
+        self.label, self.n, self.m, self.comms, self.pi_indexes = label, n, m, comms, pi_indexes
+
+
+class Prover:
+    def __init__(self, key_handle, n, m, label, pp):
+        self._key, self.n, self.m, self.label, self.pp = key_handle, n, m, label, pp
+
+    def create_proof(self, seed: int, circuit):
+        cs = Plonk()
+        circuit.synthesize(cs)
+        return self.prove_composer(cs, seed)
+
+    def prove_composer(self, cs: Plonk, seed: int):
+        proof = PlkProof()
+        pis = (PlkFr * 4096)()
+        cnt = C.c_size_t()
+        st = _bind().plk_prove(self._key, cs._h, seed, C.byref(proof), pis, 4096, C.byref(cnt))
+        if st != PLK_OK:
+            raise PlonkError(st, "create_proof")
+        return Proof(proof), [fr_int(pis[i]) for i in range(cnt.value)]
+
+    def __del__(self):
+        try:
+            if self._key:
+                _bind().plk_key_destroy(self._key)
+        except Exception:
+            pass
+
+
+class PlonkKey:
+    @staticmethod
+    def compile_with_circuit(pp: PlonkParams, label: bytes, circuit):
+        cs = Plonk()
+        circuit.synthesize(cs)
+        return PlonkKey.compile_composer(pp, label, cs)
+
+    @staticmethod
+    def compile_composer(pp: PlonkParams, label: bytes, cs: Plonk):
+        lib = _bind()
+        h = C.c_void_p()
+        _check(lib.plk_key_compile(pp._h, cs._h, label, C.byref(h)), "PlonkKey::compile")
+        n, m = C.c_uint64(), C.c_uint64()
+        comms = np.zeros((15, 13), dtype=np.uint64)
+        _check(lib.plk_key_info(h, C.byref(n), C.byref(m), _ptr(comms)), "plk_key_info")
+        _, idx = cs.public_inputs()
+        prover = Prover(h, n.value, m.value, label, pp)
+        return prover, VerifierData(label, n.value, m.value, comms, idx)

@@ -42,12 +42,15 @@ typedef enum {
   PLK_E_ARG = 2,      /* bad argument (null pointer, length > domain, bad log_n, ...) */
   PLK_E_DEVICE = 3,   /* HIP runtime error */
   PLK_E_OOM = 4,      /* device allocation failed */
-  PLK_E_NODEV = 5     /* no GPU visible / HIP unavailable */
+  PLK_E_NODEV = 5,    /* no GPU visible / HIP unavailable */
+  PLK_E_UNSUPPORTED = 6 /* circuit uses a widget this backend does not prove yet */
 } plk_status;
 
 typedef struct plk_ctx plk_ctx;
 typedef struct plk_domain plk_domain;
 typedef struct plk_srs plk_srs;
+typedef struct plk_composer plk_composer;
+typedef struct plk_key plk_key;
 
 /* ---- library / context ------------------------------------------------------------- */
 int plk_abi_version(void);
@@ -139,6 +142,70 @@ int plk_g1_sum(const plk_g1* points, size_t n, plk_g1* out);
  * number of bucket-accumulation point additions it performed. */
 int plk_srs_last_msm_stats(const plk_srs* srs, float* accumulate_ms, uint64_t* point_adds,
                            uint32_t* window_bits);
+
+/* ---- prover: Plonk composer, PlonkKey::compile, Prover::create_proof --------------------
+ * The callers of the hot path, restated on the C++ host with every O(n) step
+ * on the GPU. A constraint is one width-4 gate
+ *   q_m a b + q_l a + q_r b + q_o o + q_4 d + q_c + PI = 0   (src/lib.rs:546) plus the
+ * widget selectors; a, b, o, d are witness indices. Field order follows
+ * zksnarks::Constraint. */
+typedef struct {
+  plk_fr q_m, q_l, q_r, q_o, q_4, q_c, q_arith, q_range, q_logic, q_fixed_group_add,
+      q_variable_group_add;
+  uint32_t a, b, o, d;
+  uint32_t has_public, _pad;
+  plk_fr public_input;
+} plk_constraint;
+
+/* zksnarks Proof (src/prover/proof.rs:36-66) with ProofEvaluations in construction order
+ * (src/prover/linearization_poly.rs:117-134). */
+typedef struct {
+  plk_g1 a_comm, b_comm, c_comm, d_comm, z_comm, t_low_comm, t_mid_comm, t_high_comm, t_4_comm,
+      w_z_chall_comm, w_z_chall_w_comm;
+  plk_fr a_eval, b_eval, c_eval, d_eval, a_next_eval, b_next_eval, d_next_eval, q_arith_eval,
+      q_c_eval, q_l_eval, q_r_eval, s_sigma_1_eval, s_sigma_2_eval, s_sigma_3_eval, r_poly_eval,
+      perm_eval;
+} plk_proof;
+
+/* Plonk::initialize (src/lib.rs:121-134): zero/one witnesses, their constant gates and
+ * two rounds of dummy gates. */
+int plk_composer_create(plk_composer** out);
+int plk_composer_destroy(plk_composer* c);
+int plk_composer_size(const plk_composer* c, size_t* gates, size_t* witnesses);
+int plk_composer_append_witness(plk_composer* c, const plk_fr* value, uint32_t* wire);
+int plk_composer_witness_value(const plk_composer* c, uint32_t wire, plk_fr* value);
+int plk_composer_set_witness(plk_composer* c, uint32_t wire, const plk_fr* value);
+/* append_public (lib.rs:708-719) */
+int plk_composer_append_public(plk_composer* c, const plk_fr* value, uint32_t* wire);
+/* append_gate (lib.rs:546-550, q_arith = 1) / append_custom_gate (lib.rs:224-240) */
+int plk_composer_append_gate(plk_composer* c, const plk_constraint* s);
+int plk_composer_append_custom_gate(plk_composer* c, const plk_constraint* s);
+/* gate_add / gate_mul (lib.rs:1169-1197): q_o = -1, output evaluated and appended */
+int plk_composer_gate_eval(plk_composer* c, const plk_constraint* s, uint32_t* out_wire);
+int plk_composer_assert_equal(plk_composer* c, uint32_t a, uint32_t b);            /* :721 */
+int plk_composer_assert_equal_constant(plk_composer* c, uint32_t a, const plk_fr* constant,
+                                       const plk_fr* public_input /* nullable */);  /* :766 */
+int plk_composer_component_boolean(plk_composer* c, uint32_t a);                   /* :859 */
+/* The bench circuit: `gates` chained gates x' = x*y + x (q_m = q_l = 1, q_o = -1). */
+int plk_composer_synthetic_chain(plk_composer* c, size_t gates, uint64_t seed);
+/* Plonk::instance(): public inputs sorted by gate index, and their indexes. */
+int plk_composer_public_inputs(const plk_composer* c, plk_fr* values, uint64_t* indexes,
+                               size_t cap, size_t* count);
+
+/* PlonkKey::compile_with_circuit (src/key.rs:63-327): device-resident proving key for the
+ * circuit's structure, committed against `srs` (trimmed to next_pow2(m + 6) + 8 points).
+ * PLK_E_UNSUPPORTED for logic / curve-widget selectors (next round). */
+int plk_key_compile(plk_srs* srs, const plk_composer* circuit, const char* label, plk_key** out);
+int plk_key_destroy(plk_key* key);
+/* n (padded domain), m (gates) and the 15 verifier-key commitments in transcript order
+ * q_m q_l q_r q_o q_c q_4 q_arith q_range q_logic q_fixed_group_add q_variable_group_add
+ * s_sigma_1..4. */
+int plk_key_info(const plk_key* key, uint64_t* n, uint64_t* m, plk_g1* commitments);
+/* Prover::create_proof (src/prover.rs:67-474) for a circuit with the key's structure and
+ * its own witness values. Blinding randomness comes from `seed` (SplitMix64). Fails with
+ * PLK_E_DEGREE exactly where the reference's commit fails for an unsatisfied circuit. */
+int plk_prove(plk_key* key, const plk_composer* circuit, uint64_t seed, plk_proof* proof,
+              plk_fr* public_inputs, size_t pi_cap, size_t* pi_count);
 
 /* ---- test support ---------------------------------------------------------------- */
 /* Elementwise device field arithmetic on host arrays (used by the parity tests to pin the
