@@ -40,6 +40,14 @@ ABI_SYMBOLS = (
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
     "plk_srs_last_msm_stats", "plk_debug_field_op", "plk_commit_batch_dev",
     "plk_srs_setup_range", "plk_g1_sum",
+    # prover (dusk-plonk_amd/prover.py binds these)
+    "plk_composer_create", "plk_composer_destroy", "plk_composer_size",
+    "plk_composer_append_witness", "plk_composer_witness_value", "plk_composer_set_witness",
+    "plk_composer_append_public", "plk_composer_append_gate", "plk_composer_append_custom_gate",
+    "plk_composer_gate_eval", "plk_composer_assert_equal", "plk_composer_assert_equal_constant",
+    "plk_composer_component_boolean", "plk_composer_synthetic_chain",
+    "plk_composer_public_inputs", "plk_key_compile", "plk_key_destroy", "plk_key_info",
+    "plk_prove",
 )
 
 
