@@ -161,10 +161,15 @@ class Transcript {
       hi.v[i] = (uint32_t)b[32 + 4 * i] | ((uint32_t)b[33 + 4 * i] << 8) |
                 ((uint32_t)b[34 + 4 * i] << 16) | ((uint32_t)b[35 + 4 * i] << 24);
     }
+    // the spare-bit Montgomery multiply needs canonical inputs: 2^256 < 3r, so at most
+    // two conditional subtractions bring each half below r
+    for (int k = 0; k < 2; ++k) {
+      fe_reduce_once(lo);
+      fe_reduce_once(hi);
+    }
     Fr r2;
     for (int i = 0; i < 8; ++i) r2.v[i] = FrCfg::R2[i];
     const Fr r3 = fe_mul(r2, r2);  // R^2 * R^2 / R = R^3
-    // fe_mul(x, R^2) = x * R (Montgomery form of x) even for x >= r (< 2^256 < 2.3 r)
     return fe_add(fe_mul(lo, r2), fe_mul(hi, r3));
   }
 
