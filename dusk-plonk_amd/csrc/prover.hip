@@ -85,7 +85,8 @@ Gate default_gate() {
 
 uint32_t append_witness(plk_composer* c, const Fr& v) {
   c->witness.push_back(v);
-  c->wire_map.emplace_back();
+  c->wire_head.push_back(plk_composer::kNoWire);
+  c->wire_tail.push_back(plk_composer::kNoWire);
   return (uint32_t)(c->witness.size() - 1);
 }
 
@@ -94,7 +95,15 @@ int append_custom_gate(plk_composer* c, const Gate& g) {
     if (g.w[k] >= c->witness.size()) return PLK_E_ARG;  // permutation.rs:98 assert
   const uint32_t n = (uint32_t)c->gates.size();
   c->gates.push_back(g);
-  for (int k = 0; k < 4; ++k) c->wire_map[g.w[k]].push_back(4 * n + k);
+  for (int k = 0; k < 4; ++k) {  // add_witnesses_to_map (permutation.rs:72-91)
+    const uint32_t wire = 4 * n + k, wit = g.w[k];
+    c->wire_next.push_back(plk_composer::kNoWire);
+    if (c->wire_tail[wit] == plk_composer::kNoWire)
+      c->wire_head[wit] = wire;
+    else
+      c->wire_next[c->wire_tail[wit]] = wire;
+    c->wire_tail[wit] = wire;
+  }
   return PLK_OK;
 }
 
@@ -357,7 +366,9 @@ int plk_composer_synthetic_chain(plk_composer* c, size_t gates, uint64_t seed) {
     Rng rng{seed};
     uint32_t x = append_witness(c, rng.fr());
     c->witness.reserve(c->witness.size() + 2 * gates);
-    c->wire_map.reserve(c->wire_map.size() + 2 * gates);
+    c->wire_head.reserve(c->wire_head.size() + 2 * gates);
+    c->wire_tail.reserve(c->wire_tail.size() + 2 * gates);
+    c->wire_next.reserve(c->wire_next.size() + 4 * gates);
     c->gates.reserve(c->gates.size() + gates);
     const Fr one = fe_one<FrCfg>();
     for (size_t i = 0; i < gates; ++i) {
@@ -423,7 +434,6 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     key->m = m;
     key->n = n;
     key->k = k;
-    key->gates = cs->gates;
     // keypair.trim(additional_n) with additional_n = next_pow2(m + 6) (key.rs:81-82); the
     // trimmed SRS keeps PlonkParams' slack of 8 points
     key->n_trim = (1ull << log2_ceil(m + 6)) + 8;
@@ -451,9 +461,11 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     std::vector<uint32_t> codes(4 * n);
     for (uint64_t i = 0; i < n; ++i)
       for (uint32_t col = 0; col < 4; ++col) codes[col * n + i] = (uint32_t)(4 * i + col);
-    for (const auto& wires : cs->wire_map)
-      for (size_t j = 0; j < wires.size(); ++j) {
-        const uint32_t cur = wires[j], nxt = wires[(j + 1) % wires.size()];
+    // each witness's wires form a cycle in insertion order: wire -> next, last -> first
+    for (size_t wit = 0; wit < cs->wire_head.size(); ++wit)
+      for (uint32_t cur = cs->wire_head[wit]; cur != plk_composer::kNoWire; cur = cs->wire_next[cur]) {
+        const uint32_t nx = cs->wire_next[cur];
+        const uint32_t nxt = nx == plk_composer::kNoWire ? cs->wire_head[wit] : nx;
         codes[(cur & 3) * n + (cur >> 2)] = nxt;
       }
     DevBuf dcodes;

@@ -78,8 +78,11 @@ struct Gate {
 struct plk_composer {
   std::vector<plk::Fr> witness;
   std::vector<plk::Gate> gates;
-  // witness -> wires in insertion order (permutation.rs:21-25,72-104): wire = 4*gate + col
-  std::vector<std::vector<uint32_t>> wire_map;
+  // witness -> its wires in insertion order (permutation.rs:21-25,72-104), wire = 4*gate+col,
+  // as flat singly linked lists (no per-witness allocation): head/tail per witness, next
+  // per wire; kNoWire terminates.
+  static constexpr uint32_t kNoWire = 0xffffffffu;
+  std::vector<uint32_t> wire_head, wire_tail, wire_next;
 };
 
 struct plk_key {
@@ -91,7 +94,6 @@ struct plk_key {
   plk_domain* dom = nullptr;   // n
   plk_domain* dom8 = nullptr;  // 8n
   bool has_range = false;
-  std::vector<plk::Gate> gates;  // structure the key was compiled from (selectors, wiring)
   // device-resident proving key
   plk::DevBuf q_coef;       // 11 x n selector coefficient polys
   plk::DevBuf sel8;         // SEL_COUNT8 x 8n coset evaluations
