@@ -1,0 +1,159 @@
+// g1r.hpp — the XYZZ group law of g1.hpp over the redundant-limb field (ffr.hpp), for the
+// MSM's device stages. Same formulas (EFD g1p/shortw/xyzz madd-2008-s, add-2008-s,
+// dbl-2008-s-1, mdbl-2008-s-1, a = 0) and the same exceptional-case handling; coordinates
+// are R'-domain values in [0, 2p). Points travel through memory in the packed G1Affine /
+// G1xyzz layouts of g1.hpp (R'-domain contents).
+#pragma once
+#include "ffr.hpp"
+#include "g1.hpp"
+
+namespace plk {
+
+using RFp = Rx<FpCfg>;
+
+struct G1R {
+  RFp X, Y, ZZ, ZZZ;  // ZZ == 0 <=> infinity
+};
+
+__device__ __forceinline__ G1R g1r_infinity() {
+  G1R r;
+  r.X = rx_one<FpCfg>();
+  r.Y = rx_one<FpCfg>();
+  r.ZZ = rx_zero<FpCfg>();
+  r.ZZZ = rx_zero<FpCfg>();
+  return r;
+}
+
+__device__ __forceinline__ bool g1r_is_inf(const G1R& p) { return rx_is_zero(p.ZZ); }
+
+__device__ __forceinline__ G1R g1r_dbl(const G1R& p) {
+  if (g1r_is_inf(p)) return p;
+  const RFp U = rx_dbl(p.Y);
+  const RFp V = rx_sqr(U);
+  const RFp W = rx_mul(U, V);
+  const RFp S = rx_mul(p.X, V);
+  const RFp X2 = rx_sqr(p.X);
+  const RFp M = rx_add(rx_dbl(X2), X2);
+  G1R r;
+  r.X = rx_sub(rx_sqr(M), rx_dbl(S));
+  r.Y = rx_sub(rx_mul(M, rx_sub(S, r.X)), rx_mul(W, p.Y));
+  r.ZZ = rx_mul(V, p.ZZ);
+  r.ZZZ = rx_mul(W, p.ZZZ);
+  return r;
+}
+
+__device__ __forceinline__ G1R g1r_dbl_affine(const RFp& x, const RFp& y) {
+  const RFp U = rx_dbl(y);
+  const RFp V = rx_sqr(U);
+  const RFp W = rx_mul(U, V);
+  const RFp S = rx_mul(x, V);
+  const RFp X2 = rx_sqr(x);
+  const RFp M = rx_add(rx_dbl(X2), X2);
+  G1R r;
+  r.X = rx_sub(rx_sqr(M), rx_dbl(S));
+  r.Y = rx_sub(rx_mul(M, rx_sub(S, r.X)), rx_mul(W, y));
+  r.ZZ = V;
+  r.ZZZ = W;
+  return r;
+}
+
+// p + (x2, y2), the affine operand never infinity
+__device__ __forceinline__ G1R g1r_add_affine(const G1R& p, const RFp& x2, const RFp& y2) {
+  if (g1r_is_inf(p)) {
+    G1R r;
+    r.X = x2;
+    r.Y = y2;
+    r.ZZ = rx_one<FpCfg>();
+    r.ZZZ = rx_one<FpCfg>();
+    return r;
+  }
+  const RFp U2 = rx_mul(x2, p.ZZ);
+  const RFp S2 = rx_mul(y2, p.ZZZ);
+  const RFp P = rx_sub(U2, p.X);
+  const RFp R = rx_sub(S2, p.Y);
+  if (rx_is_zero(P)) {
+    if (rx_is_zero(R)) return g1r_dbl_affine(x2, y2);
+    return g1r_infinity();
+  }
+  const RFp PP = rx_sqr(P);
+  const RFp PPP = rx_mul(P, PP);
+  const RFp Q = rx_mul(p.X, PP);
+  G1R r;
+  r.X = rx_sub(rx_sub(rx_sqr(R), PPP), rx_dbl(Q));
+  r.Y = rx_sub(rx_mul(R, rx_sub(Q, r.X)), rx_mul(p.Y, PPP));
+  r.ZZ = rx_mul(p.ZZ, PP);
+  r.ZZZ = rx_mul(p.ZZZ, PPP);
+  return r;
+}
+
+__device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
+  if (g1r_is_inf(p)) return q;
+  if (g1r_is_inf(q)) return p;
+  const RFp U1 = rx_mul(p.X, q.ZZ);
+  const RFp U2 = rx_mul(q.X, p.ZZ);
+  const RFp S1 = rx_mul(p.Y, q.ZZZ);
+  const RFp S2 = rx_mul(q.Y, p.ZZZ);
+  const RFp P = rx_sub(U2, U1);
+  const RFp R = rx_sub(S2, S1);
+  if (rx_is_zero(P)) {
+    if (rx_is_zero(R)) return g1r_dbl(p);
+    return g1r_infinity();
+  }
+  const RFp PP = rx_sqr(P);
+  const RFp PPP = rx_mul(P, PP);
+  const RFp Q = rx_mul(U1, PP);
+  G1R r;
+  r.X = rx_sub(rx_sub(rx_sqr(R), PPP), rx_dbl(Q));
+  r.Y = rx_sub(rx_mul(R, rx_sub(Q, r.X)), rx_mul(S1, PPP));
+  r.ZZ = rx_mul(rx_mul(p.ZZ, q.ZZ), PP);
+  r.ZZZ = rx_mul(rx_mul(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+// ---- packed memory <-> limbs (16-byte loads/stores of the 48-byte coordinates) -------
+__device__ __forceinline__ RFp ld_rfp(const uint32_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  Fp x;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint4 a = q[i];
+    x.v[4 * i] = a.x;
+    x.v[4 * i + 1] = a.y;
+    x.v[4 * i + 2] = a.z;
+    x.v[4 * i + 3] = a.w;
+  }
+  return rx_unpack(x);
+}
+
+__device__ __forceinline__ void st_rfp(uint32_t* p, const RFp& r) {
+  const Fp x = rx_pack(r);
+  uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    q[i] = make_uint4(x.v[4 * i], x.v[4 * i + 1], x.v[4 * i + 2], x.v[4 * i + 3]);
+}
+
+__device__ __forceinline__ void ld_g1r_aff(const G1Affine* p, RFp& x, RFp& y) {
+  x = ld_rfp(reinterpret_cast<const uint32_t*>(p));
+  y = ld_rfp(reinterpret_cast<const uint32_t*>(p) + 12);
+}
+
+__device__ __forceinline__ G1R ld_g1r(const G1xyzz* p) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+  G1R r;
+  r.X = ld_rfp(q);
+  r.Y = ld_rfp(q + 12);
+  r.ZZ = ld_rfp(q + 24);
+  r.ZZZ = ld_rfp(q + 36);
+  return r;
+}
+
+__device__ __forceinline__ void st_g1r(G1xyzz* p, const G1R& r) {
+  uint32_t* q = reinterpret_cast<uint32_t*>(p);
+  st_rfp(q, r.X);
+  st_rfp(q + 12, r.Y);
+  st_rfp(q + 24, r.ZZ);
+  st_rfp(q + 36, r.ZZZ);
+}
+
+}  // namespace plk

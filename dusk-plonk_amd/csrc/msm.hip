@@ -29,6 +29,7 @@
 
 #include "internal.hpp"
 #include "msm_common.hpp"
+#include "g1r.hpp"
 
 namespace plk {
 
@@ -204,17 +205,17 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
   if (t >= task_off[(size_t)slot * (B + 1) + B]) return;
   const uint2 task = tasks[(size_t)slot * task_stride + t];
   sorted += (size_t)slot * sorted_stride;
-  G1xyzz acc = xyzz_infinity();
+  G1R acc = g1r_infinity();
   for (uint32_t e = task.x; e < task.x + task.y; ++e) {
     const uint32_t code = sorted[e];
     const uint32_t idx = code & 0x7fffffffu;
     if (HAS_INF && table_inf[idx]) continue;
-    Fp x, y;
-    ld_aff(&table[idx], x, y);
-    if (code & 0x80000000u) y = fe_neg(y);
-    acc = xyzz_add_affine(acc, x, y);
+    RFp x, y;
+    ld_g1r_aff(&table[idx], x, y);
+    if (code & 0x80000000u) y = rx_neg(y);
+    acc = g1r_add_affine(acc, x, y);
   }
-  st_xyzz(&partials[(size_t)slot * task_stride + t], acc);
+  st_g1r(&partials[(size_t)slot * task_stride + t], acc);
 }
 
 __global__ void __launch_bounds__(128) k_bucket_reduce(const uint32_t* __restrict__ task_off,
@@ -226,13 +227,9 @@ __global__ void __launch_bounds__(128) k_bucket_reduce(const uint32_t* __restric
   if (b >= B) return;
   task_off += (size_t)slot * (B + 1);
   partials += (size_t)slot * task_stride;
-  G1xyzz acc = xyzz_infinity();
-  for (uint32_t t = task_off[b]; t < task_off[b + 1]; ++t) {
-    G1xyzz q;
-    ld_xyzz(&partials[t], q);
-    acc = xyzz_add(acc, q);
-  }
-  st_xyzz(&buckets[(size_t)slot * B + b], acc);
+  G1R acc = g1r_infinity();
+  for (uint32_t t = task_off[b]; t < task_off[b + 1]; ++t) acc = g1r_add(acc, ld_g1r(&partials[t]));
+  st_g1r(&buckets[(size_t)slot * B + b], acc);
 }
 
 // Workgroup g owns buckets [256g, 256g+256). Thread (j, s) sums the 16 buckets
@@ -246,24 +243,20 @@ __global__ void __launch_bounds__(256) k_bitsum1(const G1xyzz* __restrict__ buck
   out += (size_t)slot * gridDim.x * nbits;
   const uint32_t tid = threadIdx.x;
   const uint32_t j = tid >> 4, s = tid & 15;
-  G1xyzz acc = xyzz_infinity();
+  G1R acc = g1r_infinity();
   if (j < nbits) {
     for (uint32_t u = 0; u < 16; ++u) {
       const uint32_t b = blockIdx.x * 256 + s * 16 + u;
-      if (b < B && (((b + 1) >> j) & 1u)) {
-        G1xyzz q;
-        ld_xyzz(&buckets[b], q);
-        acc = xyzz_add(acc, q);
-      }
+      if (b < B && (((b + 1) >> j) & 1u)) acc = g1r_add(acc, ld_g1r(&buckets[b]));
     }
   }
-  sh[tid] = acc;
+  st_g1r(&sh[tid], acc);
   __syncthreads();
   for (uint32_t h = 8; h >= 1; h >>= 1) {
-    if (s < h) sh[tid] = xyzz_add(sh[tid], sh[tid + h]);
+    if (s < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
     __syncthreads();
   }
-  if (s == 0 && j < nbits) st_xyzz(&out[blockIdx.x * nbits + j], sh[tid]);
+  if (s == 0 && j < nbits) out[blockIdx.x * nbits + j] = sh[tid];
 }
 
 // Workgroup j of slot sums in[slot][g * nbits + j] over g < G.
@@ -272,19 +265,15 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
   __shared__ G1xyzz sh[256];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
   in += (size_t)slot * G * nbits;
-  G1xyzz acc = xyzz_infinity();
-  for (uint32_t g = tid; g < G; g += 256) {
-    G1xyzz q;
-    ld_xyzz(&in[g * nbits + j], q);
-    acc = xyzz_add(acc, q);
-  }
-  sh[tid] = acc;
+  G1R acc = g1r_infinity();
+  for (uint32_t g = tid; g < G; g += 256) acc = g1r_add(acc, ld_g1r(&in[g * nbits + j]));
+  st_g1r(&sh[tid], acc);
   __syncthreads();
   for (uint32_t h = 128; h >= 1; h >>= 1) {
-    if (tid < h) sh[tid] = xyzz_add(sh[tid], sh[tid + h]);
+    if (tid < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
     __syncthreads();
   }
-  if (tid == 0) st_xyzz(&out[(size_t)slot * nbits + j], sh[0]);
+  if (tid == 0) out[(size_t)slot * nbits + j] = sh[0];
 }
 
 // flag[slot] |= any nonzero scalar in [len, check_len)  (commit degree check)
@@ -296,6 +285,23 @@ __global__ void k_any_nonzero(MsmBatch batch, uint32_t* __restrict__ flag) {
 }
 
 }  // namespace
+
+// R'-domain [0, 2p) packed coordinates (ffr.hpp) -> canonical R-domain: x * 2^-8 with the
+// R-domain product x * 2^376 / 2^384.
+static Fp fp_rx_to_r(Fp x) {
+  fe_reduce_once(x);
+  Fp k = fe_zero<FpCfg>();
+  k.v[11] = 0x01000000u;  // 2^376 (< p)
+  return fe_mul(x, k);
+}
+static G1xyzz rx_to_r_domain(const G1xyzz& p) {
+  G1xyzz r;
+  r.X = fp_rx_to_r(p.X);
+  r.Y = fp_rx_to_r(p.Y);
+  r.ZZ = fp_rx_to_r(p.ZZ);
+  r.ZZZ = fp_rx_to_r(p.ZZZ);
+  return r;
+}
 
 int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
   MsmWorkspace& w = *s->ws;
@@ -436,11 +442,12 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
       if (overall == PLK_OK) overall = PLK_E_DEGREE;
       continue;
     }
-    // host tail: sum_j 2^j T_j (Horner), then canonical affine
+    // host tail: sum_j 2^j T_j (Horner), then canonical affine. The device stages work in
+    // the R' domain (ffr.hpp) with values in [0, 2p): reduce and map back to R first.
     G1xyzz acc = xyzz_infinity();
     for (int j = (int)nbits - 1; j >= 0; --j) {
       acc = xyzz_dbl(acc);
-      acc = xyzz_add(acc, T[(size_t)k * nbits + j]);
+      acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nbits + j]));
     }
     Fp x, y;
     const bool fin = xyzz_to_affine(acc, x, y);

@@ -70,6 +70,27 @@ struct Rng {
       if (lt) return fe_to_mont(c);
     }
   }
+  // uniform Fr drawn directly as its Montgomery image (x -> xR is a bijection of Fr), so no
+  // multiply: used for the synthetic circuit's witnesses
+  Fr fr_mont() {
+    for (;;) {
+      Fr c;
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t w = next();
+        c.v[2 * i] = (uint32_t)w;
+        c.v[2 * i + 1] = (uint32_t)(w >> 32);
+      }
+      c.v[7] &= 0x7fffffffu;
+      if (c.v[7] < FrCfg::P[7]) return c;  // top word strictly below: c < r
+      if (c.v[7] == FrCfg::P[7]) {
+        for (int i = 6; i >= 0; --i)
+          if (c.v[i] != FrCfg::P[i]) {
+            if (c.v[i] < FrCfg::P[i]) return c;
+            break;
+          }
+      }
+    }
+  }
 };
 
 enum { QM = 0, QL, QR, QO, Q4, QC, QARITH, QRANGE, QLOGIC, QFIXED, QVAR };
@@ -90,7 +111,59 @@ uint32_t append_witness(plk_composer* c, const Fr& v) {
   return (uint32_t)(c->witness.size() - 1);
 }
 
-int append_custom_gate(plk_composer* c, const Gate& g) {
+// Montgomery images of the selector codes kSelZero / kSelOne / kSelMinusOne
+struct SelConsts {
+  Fr v[3];
+  SelConsts() {
+    v[0] = fe_zero<FrCfg>();
+    v[1] = fe_one<FrCfg>();
+    v[2] = fe_neg(v[1]);
+  }
+};
+const SelConsts& sel_consts() {
+  static const SelConsts k;
+  return k;
+}
+
+GateRec gate_pack(plk_composer* c, const Gate& g) {
+  const SelConsts& k = sel_consts();
+  GateRec r;
+  std::memcpy(r.w, g.w, sizeof r.w);
+  r.code = 0;
+  r.ext = (uint32_t)c->consts.size();
+  for (int q = 0; q < 11; ++q) {
+    uint32_t code = kSelPooled;
+    for (uint32_t j = 0; j < 3; ++j)
+      if (fe_eq(g.q[q], k.v[j])) {
+        code = j;
+        break;
+      }
+    if (code == kSelPooled) c->consts.push_back(g.q[q]);
+    r.code |= code << (2 * q);
+  }
+  if (g.has_pi) {
+    r.code |= kPiBit;
+    c->consts.push_back(g.pi);
+  }
+  return r;
+}
+
+Gate gate_unpack(const plk_composer* c, size_t i) {
+  const SelConsts& k = sel_consts();
+  const GateRec& r = c->gates[i];
+  Gate g;
+  std::memcpy(g.w, r.w, sizeof g.w);
+  uint32_t e = r.ext;
+  for (int q = 0; q < 11; ++q) {
+    const uint32_t code = sel_code(r.code, q);
+    g.q[q] = code == kSelPooled ? c->consts[e++] : k.v[code];
+  }
+  g.has_pi = (r.code & kPiBit) != 0;
+  g.pi = g.has_pi ? c->consts[e] : fe_zero<FrCfg>();
+  return g;
+}
+
+int push_gate(plk_composer* c, const GateRec& g) {
   for (int k = 0; k < 4; ++k)
     if (g.w[k] >= c->witness.size()) return PLK_E_ARG;  // permutation.rs:98 assert
   const uint32_t n = (uint32_t)c->gates.size();
@@ -105,6 +178,12 @@ int append_custom_gate(plk_composer* c, const Gate& g) {
     c->wire_tail[wit] = wire;
   }
   return PLK_OK;
+}
+
+int append_custom_gate(plk_composer* c, const Gate& g) {
+  for (int k = 0; k < 4; ++k)
+    if (g.w[k] >= c->witness.size()) return PLK_E_ARG;
+  return push_gate(c, gate_pack(c, g));
 }
 
 int append_gate(plk_composer* c, Gate g) {  // Constraint::arithmetic
@@ -364,25 +443,25 @@ int plk_composer_synthetic_chain(plk_composer* c, size_t gates, uint64_t seed) {
   if (!c) return PLK_E_ARG;
   try {
     Rng rng{seed};
-    uint32_t x = append_witness(c, rng.fr());
+    uint32_t x = append_witness(c, rng.fr_mont());
     c->witness.reserve(c->witness.size() + 2 * gates);
     c->wire_head.reserve(c->wire_head.size() + 2 * gates);
     c->wire_tail.reserve(c->wire_tail.size() + 2 * gates);
     c->wire_next.reserve(c->wire_next.size() + 4 * gates);
     c->gates.reserve(c->gates.size() + gates);
-    const Fr one = fe_one<FrCfg>();
+    GateRec g;
+    g.code = (kSelOne << (2 * QM)) | (kSelOne << (2 * QL)) | (kSelMinusOne << (2 * QO)) |
+             (kSelOne << (2 * QARITH));
+    g.ext = (uint32_t)c->consts.size();
+    g.w[3] = 0;  // Plonk::ZERO
     for (size_t i = 0; i < gates; ++i) {
-      const uint32_t y = append_witness(c, rng.fr());
-      Gate g = default_gate();
-      g.q[QM] = one;
-      g.q[QL] = one;
-      g.q[QARITH] = one;
-      g.q[QO] = fe_neg(one);
+      const uint32_t y = append_witness(c, rng.fr_mont());
+      const Fr& xv = c->witness[x];
+      const Fr o = fe_add(fe_mul(xv, c->witness[y]), xv);
       g.w[0] = x;
       g.w[1] = y;
-      const Fr o = fe_add(fe_mul(c->witness[x], c->witness[y]), c->witness[x]);
       g.w[2] = append_witness(c, o);
-      if (append_custom_gate(c, g) != PLK_OK) return PLK_E_ARG;
+      if (push_gate(c, g) != PLK_OK) return PLK_E_ARG;
       x = g.w[2];
     }
     return PLK_OK;
@@ -405,9 +484,9 @@ int plk_composer_public_inputs(const plk_composer* c, plk_fr* values, uint64_t* 
   if (!c || !count) return PLK_E_ARG;
   size_t k = 0;
   for (size_t i = 0; i < c->gates.size(); ++i) {
-    if (!c->gates[i].has_pi) continue;
+    if (!(c->gates[i].code & kPiBit)) continue;
     if (k < cap) {
-      if (values) values[k] = fr_to(c->gates[i].pi);
+      if (values) values[k] = fr_to(gate_unpack(c, i).pi);
       if (indexes) indexes[k] = i;
     }
     ++k;
@@ -438,7 +517,8 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     // trimmed SRS keeps PlonkParams' slack of 8 points
     key->n_trim = (1ull << log2_ceil(m + 6)) + 8;
     if (k + 3 > 27) return PLK_E_ARG;
-    for (const Gate& g : cs->gates) {
+    for (uint64_t i = 0; i < m; ++i) {
+      const Gate g = gate_unpack(cs, i);
       if (!fe_is_zero(g.q[QLOGIC]) || !fe_is_zero(g.q[QFIXED]) || !fe_is_zero(g.q[QVAR]))
         return PLK_E_UNSUPPORTED;  // logic / curve widgets: next round
       if (!fe_is_zero(g.q[QRANGE])) key->has_range = true;
@@ -449,8 +529,10 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
 
     // 1. selectors padded to n (key.rs:89-119) -> idft (key.rs:121-131)
     std::vector<Fr> host(11 * n, fe_zero<FrCfg>());
-    for (uint64_t i = 0; i < m; ++i)
-      for (int q = 0; q < 11; ++q) host[q * n + i] = cs->gates[i].q[q];
+    for (uint64_t i = 0; i < m; ++i) {
+      const Gate g = gate_unpack(cs, i);
+      for (int q = 0; q < 11; ++q) host[q * n + i] = g.q[q];
+    }
     TRY(key->q_coef.alloc(11 * n * sizeof(Fr)));
     PLK_HIP_TRY(hipMemcpyAsync(key->q_coef.ptr, host.data(), 11 * n * sizeof(Fr),
                                hipMemcpyHostToDevice, s));
@@ -597,7 +679,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     // public inputs (prover.rs:90-105)
     std::vector<std::pair<uint64_t, Fr>> pis;
     for (uint64_t i = 0; i < m; ++i)
-      if (cs->gates[i].has_pi) pis.emplace_back(i, cs->gates[i].pi);
+      if (cs->gates[i].code & kPiBit) pis.emplace_back(i, gate_unpack(cs, i).pi);
     for (auto& p : pis) tr.append_scalar("pi", p.second);
     if (pi_count) *pi_count = pis.size();
     if (public_inputs)

@@ -73,11 +73,26 @@ struct Gate {
   Fr pi;
 };
 
+// The composer stores a gate as 24 bytes instead of Gate's 416: the four wires, a 2-bit
+// code per selector (kSelZero / kSelOne / kSelMinusOne / kSelPooled) with bit kPiBit set
+// when the gate carries a public input, and `ext`, the index in plk_composer::consts of
+// the gate's pooled selectors (in selector order) followed by its PI value. Circuits are
+// dominated by 0/±1 selectors, so synthesis writes ~17x fewer bytes per gate.
+enum : uint32_t { kSelZero = 0, kSelOne = 1, kSelMinusOne = 2, kSelPooled = 3 };
+constexpr uint32_t kPiBit = 1u << 22;
+struct GateRec {
+  uint32_t w[4];
+  uint32_t code;
+  uint32_t ext;
+};
+inline uint32_t sel_code(uint32_t code, int q) { return (code >> (2 * q)) & 3u; }
+
 }  // namespace plk
 
 struct plk_composer {
   std::vector<plk::Fr> witness;
-  std::vector<plk::Gate> gates;
+  std::vector<plk::GateRec> gates;
+  std::vector<plk::Fr> consts;  // pooled selector / PI values (see GateRec)
   // witness -> its wires in insertion order (permutation.rs:21-25,72-104), wire = 4*gate+col,
   // as flat singly linked lists (no per-witness allocation): head/tail per witness, next
   // per wire; kNoWire terminates.

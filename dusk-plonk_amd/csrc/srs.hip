@@ -9,6 +9,7 @@
 
 #include "internal.hpp"
 #include "msm_common.hpp"
+#include "ffr.hpp"
 
 namespace plk {
 
@@ -80,6 +81,15 @@ __global__ void __launch_bounds__(128) k_batch_affine(const G1xyzz* __restrict__
   }
 }
 
+// The accumulation reads the table in the R' domain of ffr.hpp: x -> x * 2^8 (canonical).
+__global__ void __launch_bounds__(256) k_table_to_rx(G1Affine* __restrict__ tab, uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  Fp x, y;
+  ld_aff(&tab[i], x, y);
+  st_aff(&tab[i], fe_to_rx_domain(x), fe_to_rx_domain(y));
+}
+
 }  // namespace
 
 // Window size for an SRS of n points (bucket count 2^(c-1); table W*n).
@@ -112,6 +122,11 @@ int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
                        temp.as<G1xyzz>(), (uint64_t)n, pref.as<Fp>(), tab + w * n, tinf + w * n);
     PLK_HIP_TRY(hipGetLastError());
   }
+  // table holds R-domain points up to here (each window doubles the previous one); the
+  // MSM reads it in the R' domain
+  hipLaunchKernelGGL(k_table_to_rx, dim3(cdiv((uint64_t)s->windows * n, 256)), dim3(256), 0, stream,
+                     tab, (uint64_t)s->windows * n);
+  PLK_HIP_TRY(hipGetLastError());
   PLK_HIP_TRY(hipStreamSynchronize(stream));
   s->ws.reset(new MsmWorkspace());
   return ws_reserve(s, n, 1);
