@@ -89,7 +89,7 @@ int plk_ctx_destroy(plk_ctx* ctx) {
   if (!ctx) return PLK_E_ARG;
   {
     DeviceGuard g(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    (void)stream_wait(ctx->stream);
     ctx->domains.clear();
     (void)hipStreamDestroy(ctx->stream);
   }
@@ -108,7 +108,7 @@ int plk_ctx_synchronize(plk_ctx* ctx) {
   PLK_API_BEGIN
   if (!ctx) return PLK_E_ARG;
   DeviceGuard g(ctx->device);
-  PLK_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  PLK_HIP_TRY(stream_wait(ctx->stream));
   return PLK_OK;
   PLK_API_END
 }
@@ -154,7 +154,7 @@ int plk_domain_elements(const plk_domain* d, plk_fr* out) {
   DeviceGuard g(d->ctx->device);
   PLK_HIP_TRY(hipMemcpyAsync(out, d->tw_fwd.ptr, d->n * sizeof(Fr), hipMemcpyDeviceToHost,
                              d->ctx->stream));
-  PLK_HIP_TRY(hipStreamSynchronize(d->ctx->stream));
+  PLK_HIP_TRY(stream_wait(d->ctx->stream));
   return PLK_OK;
   PLK_API_END
 }
@@ -169,7 +169,7 @@ int plk_domain_vanishing_over_coset(const plk_domain* dc, uint64_t poly_degree, 
   if ((st = ntt_vanishing(d, poly_degree, d->io.as<Fr>(), d->ctx->stream))) return st;
   PLK_HIP_TRY(hipMemcpyAsync(out, d->io.ptr, d->n * sizeof(Fr), hipMemcpyDeviceToHost,
                              d->ctx->stream));
-  PLK_HIP_TRY(hipStreamSynchronize(d->ctx->stream));
+  PLK_HIP_TRY(stream_wait(d->ctx->stream));
   return PLK_OK;
   PLK_API_END
 }
@@ -188,7 +188,7 @@ int plk_ntt(plk_domain* d, plk_fr* inout, size_t len_in, int dir, int coset) {
   if ((st = ntt_run(d, d->io.as<Fr>(), d->io.as<Fr>(), len_in, dir, coset, nullptr, s, 1)))
     return st;
   PLK_HIP_TRY(hipMemcpyAsync(inout, d->io.ptr, d->n * sizeof(Fr), hipMemcpyDeviceToHost, s));
-  PLK_HIP_TRY(hipStreamSynchronize(s));
+  PLK_HIP_TRY(stream_wait(s));
   return PLK_OK;
   PLK_API_END
 }
@@ -252,7 +252,7 @@ int plk_srs_points(const plk_srs* s, size_t start, size_t count, plk_g1* out) {
   PLK_HIP_TRY(hipMemcpyAsync(pts.data(), s->points.as<G1Affine>() + start, count * sizeof(G1Affine),
                              hipMemcpyDeviceToHost, st));
   PLK_HIP_TRY(hipMemcpyAsync(inf.data(), s->inf.as<uint8_t>() + start, count, hipMemcpyDeviceToHost, st));
-  PLK_HIP_TRY(hipStreamSynchronize(st));
+  PLK_HIP_TRY(stream_wait(st));
   for (size_t i = 0; i < count; ++i) g1_to_abi(pts[i], inf[i], &out[i]);
   return PLK_OK;
   PLK_API_END
@@ -320,7 +320,7 @@ int plk_srs_destroy(plk_srs* s) {
   PLK_API_BEGIN
   if (!s) return PLK_E_ARG;
   DeviceGuard g(s->ctx->device);
-  (void)hipStreamSynchronize(s->ctx->stream);
+  (void)stream_wait(s->ctx->stream);
   delete s;
   return PLK_OK;
   PLK_API_END

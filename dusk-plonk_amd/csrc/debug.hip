@@ -36,7 +36,7 @@ int run(plk_ctx* ctx, int op, const uint64_t* a, const uint64_t* b, uint64_t* ou
                      da.as<Fe<C>>(), db.as<Fe<C>>(), dout.as<Fe<C>>(), (uint64_t)n);
   PLK_HIP_TRY(hipGetLastError());
   PLK_HIP_TRY(hipMemcpyAsync(out, dout.ptr, bytes, hipMemcpyDeviceToHost, s));
-  PLK_HIP_TRY(hipStreamSynchronize(s));
+  PLK_HIP_TRY(stream_wait(s));
   return PLK_OK;
 }
 

@@ -31,6 +31,20 @@ struct DevBuf {
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), bytes(o.bytes) {
+    o.ptr = nullptr;
+    o.bytes = 0;
+  }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      if (ptr) (void)hipFree(ptr);
+      ptr = o.ptr;
+      bytes = o.bytes;
+      o.ptr = nullptr;
+      o.bytes = 0;
+    }
+    return *this;
+  }
   ~DevBuf() {
     if (ptr) (void)hipFree(ptr);
   }
@@ -66,10 +80,12 @@ struct plk_domain {
   uint32_t log_n = 0;
   uint64_t n = 0;
   plk::Fr omega, omega_inv, n_inv, g, g_inv;  // Montgomery form (host copies)
-  plk::DevBuf tw_fwd;        // w^e, e < n
-  plk::DevBuf tw_inv;        // w^-e, e < n
-  plk::DevBuf coset_pow;     // g^e, e < n
-  plk::DevBuf icoset_scale;  // n^-1 * g^-e, e < n
+  plk::DevBuf tw_fwd;        // w^e, e < n (R domain: the domain elements)
+  plk::DevBuf tw_fwd_rx;     // w^e, R' domain (ffr.hpp), read by the NTT passes
+  plk::DevBuf tw_inv;        // w^-e, e < n (R' domain)
+  plk::DevBuf coset_pow;     // g^e, e < n (R' domain)
+  plk::DevBuf icoset_scale;  // n^-1 * g^-e, e < n (R' domain)
+  std::vector<plk::DevBuf> pass_tw_fwd, pass_tw_inv;  // per pass q > 0: w_{Rp}^{jk} [j][k] (R')
   plk::DevBuf scratch;       // 2n elements (default scratch for plk_ntt_dev)
   plk::DevBuf io;            // n elements (host-buffer entry points stage through it)
   std::vector<plk::NttPass> plan;
@@ -107,6 +123,53 @@ struct plk_ctx {
 };
 
 namespace plk {
+// Page-locked host buffer: the prover's host<->device transfers go through these. A
+// pageable hipMemcpy pins and unpins its pages on every call, and the page-table and
+// TLB-shootdown work that comes with it slowed a concurrent composer synthesis ~1.6x.
+struct PinnedBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  ~PinnedBuf() {
+    if (ptr) (void)hipHostFree(ptr);
+  }
+  int alloc(size_t b) {
+    if (ptr && bytes >= b) return PLK_OK;
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    if (b == 0) return PLK_OK;
+    const hipError_t e = hipHostMalloc(&ptr, b, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      ptr = nullptr;
+      last_hip_error() = e;
+      return e == hipErrorOutOfMemory ? PLK_E_OOM : PLK_E_DEVICE;
+    }
+    bytes = b;
+    return PLK_OK;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(ptr);
+  }
+};
+
+// Host wait for all work queued on `s`, blocking in the driver instead of spinning: the
+// prover's host thread waits at every commitment, and a spinning wait steals the core a
+// concurrent composer synthesis (or any other host work) runs on. One event per thread.
+inline hipError_t stream_wait(hipStream_t s) {
+  thread_local hipEvent_t ev = nullptr;
+  if (!ev) {
+    const hipError_t e = hipEventCreateWithFlags(&ev, hipEventBlockingSync | hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  const hipError_t e = hipEventRecord(ev, s);
+  if (e != hipSuccess) return e;
+  return hipEventSynchronize(ev);
+}
+
 // RAII device guard
 struct DeviceGuard {
   int prev = -1;

@@ -205,14 +205,24 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
   if (t >= task_off[(size_t)slot * (B + 1) + B]) return;
   const uint2 task = tasks[(size_t)slot * task_stride + t];
   sorted += (size_t)slot * sorted_stride;
+  // software-pipelined: the next entry's index and point are loaded before the current
+  // mixed add, so the two dependent loads overlap the ~6k-instruction madd (+8%,
+  // tools/ubench_acc.hip)
   G1R acc = g1r_infinity();
-  for (uint32_t e = task.x; e < task.x + task.y; ++e) {
-    const uint32_t code = sorted[e];
-    const uint32_t idx = code & 0x7fffffffu;
-    if (HAS_INF && table_inf[idx]) continue;
-    RFp x, y;
-    ld_g1r_aff(&table[idx], x, y);
-    if (code & 0x80000000u) y = rx_neg(y);
+  const uint32_t end = task.x + task.y;
+  uint32_t code = task.y ? sorted[task.x] : 0u;
+  Fp px, py;
+  ld_aff(&table[code & 0x7fffffffu], px, py);
+  for (uint32_t e = task.x; e < end; ++e) {
+    const uint32_t cur = code;
+    const RFp x = rx_unpack(px);
+    RFp y = rx_unpack(py);
+    if (e + 1 < end) {
+      code = sorted[e + 1];
+      ld_aff(&table[code & 0x7fffffffu], px, py);
+    }
+    if (HAS_INF && table_inf[cur & 0x7fffffffu]) continue;
+    if (cur & 0x80000000u) y = rx_neg(y);
     acc = g1r_add_affine(acc, x, y);
   }
   st_g1r(&partials[(size_t)slot * task_stride + t], acc);
@@ -419,14 +429,17 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
                      G, nbits, w.bits2.as<G1xyzz>());
   PLK_HIP_TRY(hipGetLastError());
 
-  std::vector<G1xyzz> T((size_t)slots * nbits);
-  std::vector<uint32_t> flag(slots), ent(slots);
-  PLK_HIP_TRY(hipMemcpy2DAsync(ent.data(), 4, w.offsets.as<uint32_t>() + B, (B + 1) * 4, 4, slots,
+  const size_t t_count = (size_t)slots * nbits;
+  if ((st = w.host_out.alloc(t_count * sizeof(G1xyzz) + 2 * slots * sizeof(uint32_t)))) return st;
+  G1xyzz* T = w.host_out.as<G1xyzz>();
+  uint32_t* flag = reinterpret_cast<uint32_t*>(T + t_count);
+  uint32_t* ent = flag + slots;
+  PLK_HIP_TRY(hipMemcpy2DAsync(ent, 4, w.offsets.as<uint32_t>() + B, (B + 1) * 4, 4, slots,
                                hipMemcpyDeviceToHost, stream));
-  PLK_HIP_TRY(hipMemcpyAsync(T.data(), w.bits2.ptr, T.size() * sizeof(G1xyzz),
-                             hipMemcpyDeviceToHost, stream));
-  PLK_HIP_TRY(hipMemcpyAsync(flag.data(), w.flag.ptr, slots * 4, hipMemcpyDeviceToHost, stream));
-  PLK_HIP_TRY(hipStreamSynchronize(stream));
+  PLK_HIP_TRY(hipMemcpyAsync(T, w.bits2.ptr, t_count * sizeof(G1xyzz), hipMemcpyDeviceToHost,
+                             stream));
+  PLK_HIP_TRY(hipMemcpyAsync(flag, w.flag.ptr, slots * 4, hipMemcpyDeviceToHost, stream));
+  PLK_HIP_TRY(stream_wait(stream));
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, w.ev0, w.ev1) == hipSuccess) s->last_accumulate_ms = ms;
   s->last_point_adds = 0;

@@ -14,6 +14,7 @@
 // (or n^-1 g^-e) post-scale into the last pass' stores.
 //
 // HBM traffic per transform: P * 2 * N * 32 B (P = 3 at N = 2^20..2^24).
+#include "ffr.hpp"
 #include "internal.hpp"
 
 namespace plk {
@@ -42,20 +43,43 @@ __device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
   return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0u;
 }
 
+// LDS holds the R-point columns as limb planes of the redundant Fr form (ffr.hpp):
+// plane l of element idx at base[l * stride + idx], so each limb access is one
+// conflict-free ds_read_b32 / ds_write_b32 across the wave.
+using RFr = Rx<FrCfg>;
+constexpr int kL = RxShape<FrCfg>::L;
+
+__device__ __forceinline__ RFr lds_ld(const uint32_t* base, uint32_t stride, uint32_t idx) {
+  RFr r;
+#pragma unroll
+  for (int l = 0; l < kL; ++l) r.v[l] = base[l * stride + idx];
+  return r;
+}
+
+__device__ __forceinline__ void lds_st(uint32_t* base, uint32_t stride, uint32_t idx, const RFr& v) {
+#pragma unroll
+  for (int l = 0; l < kL; ++l) base[l * stride + idx] = v.v[l];
+}
+
+__device__ __forceinline__ RFr ld_rfr(const Fr* p) { return rx_unpack(ld_fr(p)); }
+
 // One Stockham pass. PRE: 0 none, 1 multiply input e by pre[e] (coset g^e).
 // POST: 0 none, 1 multiply by post_scalar, 2 multiply output e by post[e].
+// Data buffers are R-domain (canonical in and out); tw / pre / post / post_scalar are
+// R'-domain (ffr.hpp), so every product data x table stays in the R domain.
 template <int PRE, int POST>
 __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                   const Fr* __restrict__ tw,
+                                                  const Fr* __restrict__ ptw,
                                                   const Fr* __restrict__ pre,
                                                   const Fr* __restrict__ post, Fr post_scalar,
                                                   uint32_t log_n, uint32_t lp, uint32_t lr,
                                                   uint32_t lt, uint64_t len_in, uint64_t n_stride) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  Fr* data = reinterpret_cast<Fr*>(smem);
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const uint32_t R = 1u << lr, T = 1u << lt, p = 1u << lp;
-  const uint32_t E = R << lt;
-  Fr* twl = data + E;  // R/2 inner twiddles w_R^x
+  const uint32_t E = R << lt, H = R >> 1;
+  uint32_t* data = smem32;          // kL planes of E
+  uint32_t* twl = smem32 + kL * E;  // kL planes of R/2 inner twiddles w_R^x
 
   const size_t voff = (size_t)blockIdx.y * n_stride;
   in += voff;
@@ -65,23 +89,23 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   const uint32_t nr_log = log_n - lr;  // log2(N/R)
   const uint32_t i0 = blockIdx.x << lt;
 
-  for (uint32_t x = tid; x < (R >> 1); x += bd) st_fr(&twl[x], ld_fr(&tw[(size_t)x << nr_log]));
+  for (uint32_t x = tid; x < H; x += bd) lds_st(twl, H, x, ld_rfr(&tw[(size_t)x << nr_log]));
 
-  const uint32_t tw_shift = log_n - lr - lp;  // w_{Rp}^{jk} = w_N^{jk * N/(Rp)}
   for (uint32_t e = tid; e < E; e += bd) {
     const uint32_t t = e & (T - 1), j = e >> lt;
     const uint32_t i = i0 + t;
     const size_t g = (size_t)i + ((size_t)j << nr_log);
-    Fr v;
+    RFr v;
     if (g < len_in) {
-      v = ld_fr(&in[g]);
-      if (PRE == 1) v = fe_mul(v, ld_fr(&pre[g]));
+      v = ld_rfr(&in[g]);
+      if (PRE == 1) v = rx_mul(v, ld_rfr(&pre[g]));
     } else {
-      v = fe_zero<FrCfg>();
+      v = rx_zero<FrCfg>();
     }
     const uint32_t k = i & (p - 1);
-    if (j != 0 && k != 0) v = fe_mul(v, ld_fr(&tw[(size_t)(j * k) << tw_shift]));
-    st_fr(&data[(j << lt) + t], v);
+    // inter-pass twiddle w_{Rp}^{jk} from the pass table laid out [j][k] (coalesced in k)
+    if (j != 0 && k != 0) v = rx_mul(v, ld_rfr(&ptw[((size_t)j << lp) + k]));
+    lds_st(data, E, (j << lt) + t, v);
   }
   __syncthreads();
 
@@ -92,12 +116,12 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       const uint32_t t = b & (T - 1), jb = b >> lt;
       const uint32_t r = jb & (h - 1);
       const uint32_t j1 = ((jb >> lh) << (lh + 1)) + r, j2 = j1 + h;
-      const Fr a = ld_fr(&data[(j1 << lt) + t]);
-      const Fr c = ld_fr(&data[(j2 << lt) + t]);
-      st_fr(&data[(j1 << lt) + t], fe_add(a, c));
-      Fr d = fe_sub(a, c);
-      if (r != 0) d = fe_mul(d, ld_fr(&twl[r << (lr - 1 - lh)]));
-      st_fr(&data[(j2 << lt) + t], d);
+      const RFr a = lds_ld(data, E, (j1 << lt) + t);
+      const RFr c = lds_ld(data, E, (j2 << lt) + t);
+      lds_st(data, E, (j1 << lt) + t, rx_add(a, c));
+      RFr d = rx_sub(a, c);
+      if (r != 0) d = rx_mul(d, lds_ld(twl, H, r << (lr - 1 - lh)));
+      lds_st(data, E, (j2 << lt) + t, d);
     }
     __syncthreads();
   }
@@ -115,11 +139,28 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
     const uint32_t i = i0 + t;
     const uint32_t k = i & (p - 1);
     const size_t pos = ((size_t)(i - k) << lr) + k + ((size_t)m << lp);
-    Fr v = ld_fr(&data[(bitrev(m, lr) << lt) + t]);
-    if (POST == 1) v = fe_mul(v, post_scalar);
-    if (POST == 2) v = fe_mul(v, ld_fr(&post[pos]));
-    st_fr(&out[pos], v);
+    RFr v = lds_ld(data, E, (bitrev(m, lr) << lt) + t);
+    if (POST == 1) v = rx_mul(v, rx_unpack(post_scalar));
+    if (POST == 2) v = rx_mul(v, ld_rfr(&post[pos]));
+    st_fr(&out[pos], rx_pack_canonical(v));
   }
+}
+
+// pass twiddles: out[(j << lp) + k] = w_N^{(j k) << shift} for j < R, k < p (R' domain;
+// tw is the R'-domain power table of the same direction)
+__global__ void k_pass_twiddles(const Fr* __restrict__ tw, Fr* __restrict__ out, uint32_t lp,
+                                uint32_t lr, uint32_t shift) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (1ull << (lp + lr))) return;
+  const uint64_t j = e >> lp, k = e & ((1ull << lp) - 1);
+  st_fr(&out[e], ld_fr(&tw[(j * k) << shift]));
+}
+
+// in-place R -> R' domain conversion of a table (ffr.hpp)
+__global__ void k_table_to_rx(const Fr* in, Fr* out, uint64_t n) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  st_fr(&out[e], fe_to_rx_domain(ld_fr(&in[e])));
 }
 
 // table[e] = base^e * scale for e < n (exact powers; one pow per element)
@@ -208,8 +249,33 @@ int ntt_build_domain(plk_domain* d) {
   hipLaunchKernelGGL(k_power_table, dim3(nb), dim3(bs), 0, s, d->coset_pow.as<Fr>(), d->g, one, n);
   hipLaunchKernelGGL(k_power_table, dim3(nb), dim3(bs), 0, s, d->icoset_scale.as<Fr>(), d->g_inv,
                      d->n_inv, n);
+  // the pass kernel multiplies R-domain data by R'-domain tables (ffr.hpp)
+  if ((st = d->tw_fwd_rx.alloc(n * sizeof(Fr)))) return st;
+  hipLaunchKernelGGL(k_table_to_rx, dim3(nb), dim3(bs), 0, s, d->tw_fwd.as<Fr>(), d->tw_fwd_rx.as<Fr>(), n);
+  hipLaunchKernelGGL(k_table_to_rx, dim3(nb), dim3(bs), 0, s, d->tw_inv.as<Fr>(), d->tw_inv.as<Fr>(), n);
+  hipLaunchKernelGGL(k_table_to_rx, dim3(nb), dim3(bs), 0, s, d->coset_pow.as<Fr>(), d->coset_pow.as<Fr>(), n);
+  hipLaunchKernelGGL(k_table_to_rx, dim3(nb), dim3(bs), 0, s, d->icoset_scale.as<Fr>(),
+                     d->icoset_scale.as<Fr>(), n);
   PLK_HIP_TRY(hipGetLastError());
-  PLK_HIP_TRY(hipStreamSynchronize(s));
+  // per-pass inter-pass twiddle tables (passes after the first), both directions
+  d->pass_tw_fwd.clear();
+  d->pass_tw_inv.clear();
+  d->pass_tw_fwd.resize(d->plan.size());
+  d->pass_tw_inv.resize(d->plan.size());
+  for (size_t q = 1; q < d->plan.size(); ++q) {
+    const NttPass& ps = d->plan[q];
+    const uint64_t cnt = 1ull << (ps.lp + ps.lr);
+    const uint32_t shift = d->log_n - ps.lr - ps.lp;
+    if ((st = d->pass_tw_fwd[q].alloc(cnt * sizeof(Fr)))) return st;
+    if ((st = d->pass_tw_inv[q].alloc(cnt * sizeof(Fr)))) return st;
+    const uint32_t pb = (uint32_t)((cnt + bs - 1) / bs);
+    hipLaunchKernelGGL(k_pass_twiddles, dim3(pb), dim3(bs), 0, s, d->tw_fwd_rx.as<Fr>(),
+                       d->pass_tw_fwd[q].as<Fr>(), ps.lp, ps.lr, shift);
+    hipLaunchKernelGGL(k_pass_twiddles, dim3(pb), dim3(bs), 0, s, d->tw_inv.as<Fr>(),
+                       d->pass_tw_inv[q].as<Fr>(), ps.lp, ps.lr, shift);
+  }
+  PLK_HIP_TRY(hipGetLastError());
+  PLK_HIP_TRY(stream_wait(s));
   return PLK_OK;
 }
 
@@ -235,7 +301,8 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
   const size_t P = d->plan.size();
   Fr* s1 = scratch;
   Fr* s2 = scratch + n * count;
-  const Fr* tw = dir > 0 ? d->tw_fwd.as<Fr>() : d->tw_inv.as<Fr>();
+  const Fr* tw = dir > 0 ? d->tw_fwd_rx.as<Fr>() : d->tw_inv.as<Fr>();
+  const Fr n_inv_rx = fe_to_rx_domain(d->n_inv);
   const Fr* src = in;
   for (size_t q = 0; q < P; ++q) {
     const NttPass& ps = d->plan[q];
@@ -246,14 +313,16 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
     if (bd < 64) bd = 64;
     if (bd > 256) bd = 256;
     const uint32_t blocks = (uint32_t)(n >> (ps.lr + ps.lt));
-    const size_t lds = ((size_t)E + (1u << ps.lr) / 2) * sizeof(Fr);
+    const size_t lds = ((size_t)E + (1u << ps.lr) / 2) * kL * sizeof(uint32_t);
     const int pre = (first && dir > 0 && coset) ? 1 : 0;
     const int post = (last && dir < 0) ? (coset ? 2 : 1) : 0;
     const uint64_t lin = first ? len_in : n;
     dim3 grid(blocks, count);
+    const Fr* ptw = q == 0 ? nullptr
+                           : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
 #define PLK_LAUNCH(PRE, POST)                                                                 \
-  hipLaunchKernelGGL((k_ntt_pass<PRE, POST>), grid, dim3(bd), lds, stream, src, dst, tw,     \
-                     d->coset_pow.as<Fr>(), d->icoset_scale.as<Fr>(), d->n_inv, d->log_n,   \
+  hipLaunchKernelGGL((k_ntt_pass<PRE, POST>), grid, dim3(bd), lds, stream, src, dst, tw, ptw, \
+                     d->coset_pow.as<Fr>(), d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n,   \
                      ps.lp, ps.lr, ps.lt, lin, (uint64_t)n)
     if (pre == 0 && post == 0) PLK_LAUNCH(0, 0);
     else if (pre == 1 && post == 0) PLK_LAUNCH(1, 0);

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "internal.hpp"
@@ -300,10 +301,11 @@ int key_commit(plk_key* key, const std::vector<const Fr*>& ptrs, const std::vect
 }
 
 Fr d2h_fr(const Fr* p, hipStream_t s) {
-  Fr v;
-  (void)hipMemcpyAsync(&v, p, sizeof(Fr), hipMemcpyDeviceToHost, s);
-  (void)hipStreamSynchronize(s);
-  return v;
+  thread_local PinnedBuf pin;
+  if (pin.alloc(sizeof(Fr)) != PLK_OK) return fe_zero<FrCfg>();
+  (void)hipMemcpyAsync(pin.ptr, p, sizeof(Fr), hipMemcpyDeviceToHost, s);
+  (void)stream_wait(s);
+  return *pin.as<Fr>();
 }
 
 }  // namespace
@@ -329,10 +331,31 @@ __global__ void k_sigma_values(const uint32_t* __restrict__ codes, const Fr* __r
 extern "C" {
 
 // ----------------------------------------------------------------------- composer
+// Composer storage pool: a proof server synthesizes a fresh composer per proof (as
+// create_proof does, prover.rs:76-78); reusing the vectors of destroyed composers (clear()
+// keeps capacity) avoids re-faulting ~120 bytes of fresh pages per gate every proof.
+namespace {
+std::mutex g_pool_mu;
+std::vector<std::unique_ptr<plk_composer>> g_pool;
+constexpr size_t kPoolMax = 2;
+
+std::unique_ptr<plk_composer> composer_from_pool() {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_pool.empty()) {
+      std::unique_ptr<plk_composer> c = std::move(g_pool.back());
+      g_pool.pop_back();
+      return c;
+    }
+  }
+  return std::unique_ptr<plk_composer>(new plk_composer());
+}
+}  // namespace
+
 int plk_composer_create(plk_composer** out) {
   try {
     if (!out) return PLK_E_ARG;
-    std::unique_ptr<plk_composer> c(new plk_composer());
+    std::unique_ptr<plk_composer> c = composer_from_pool();
     // Plonk::initialize (lib.rs:121-134)
     const uint32_t zero = append_witness(c.get(), fe_zero<FrCfg>());
     const uint32_t one = append_witness(c.get(), fe_one<FrCfg>());
@@ -348,7 +371,16 @@ int plk_composer_create(plk_composer** out) {
 }
 
 int plk_composer_destroy(plk_composer* c) {
-  delete c;
+  if (!c) return PLK_OK;
+  std::unique_ptr<plk_composer> h(c);
+  h->witness.clear();
+  h->gates.clear();
+  h->consts.clear();
+  h->wire_head.clear();
+  h->wire_tail.clear();
+  h->wire_next.clear();
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if (g_pool.size() < kPoolMax) g_pool.push_back(std::move(h));
   return PLK_OK;
 }
 
@@ -604,7 +636,7 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
       for (int c = 0; c < 4; ++c) idx[c * n + i] = cs->gates[i].w[c];
     TRY(key->wire_idx.alloc(4 * n * 4));
     PLK_HIP_TRY(hipMemcpyAsync(key->wire_idx.ptr, idx.data(), 4 * n * 4, hipMemcpyHostToDevice, s));
-    PLK_HIP_TRY(hipStreamSynchronize(s));
+    PLK_HIP_TRY(stream_wait(s));
     *out = key.release();
     return PLK_OK;
   } catch (const std::bad_alloc&) {
@@ -617,7 +649,7 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
 int plk_key_destroy(plk_key* key) {
   if (!key) return PLK_E_ARG;
   DeviceGuard g(key->ctx->device);
-  (void)hipStreamSynchronize(key->ctx->stream);
+  (void)stream_wait(key->ctx->stream);
   delete key;
   return PLK_OK;
 }
@@ -686,8 +718,20 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       for (size_t i = 0; i < pis.size() && i < pi_cap; ++i) public_inputs[i] = fr_to(pis[i].second);
 
     // ---- round 1: wires -> idft -> blind(1) -> commit (prover.rs:107-158)
-    PLK_HIP_TRY(hipMemcpyAsync(key->witness.ptr, cs->witness.data(), cs->witness.size() * sizeof(Fr),
-                               hipMemcpyHostToDevice, s));
+    {  // witness upload through pinned staging, in chunks: the CPU copy of chunk i+1
+       // overlaps the DMA of chunk i (the previous proof's DMA finished at its last wait)
+      const size_t bytes = cs->witness.size() * sizeof(Fr);
+      TRY(key->pin_witness.alloc(bytes));
+      const size_t chunk = 8u << 20;
+      const char* src = reinterpret_cast<const char*>(cs->witness.data());
+      char* pin = key->pin_witness.as<char>();
+      char* dst = key->witness.as<char>();
+      for (size_t off = 0; off < bytes; off += chunk) {
+        const size_t len = std::min(chunk, bytes - off);
+        std::memcpy(pin + off, src + off, len);
+        PLK_HIP_TRY(hipMemcpyAsync(dst + off, pin + off, len, hipMemcpyHostToDevice, s));
+      }
+    }
     Fr* wl = key->wires_lag.as<Fr>();
     Fr* wc = key->wires_coef.as<Fr>();
     TRY(pk_gather_wires(key->witness.as<Fr>(), key->wire_idx.as<uint32_t>(), m, n, wl, s));
@@ -741,8 +785,14 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     (void)tr.challenge_scalar("variable base separation challenge");
     Fr* pil = key->pi_lag.as<Fr>();
     PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
-    for (auto& p : pis)
-      PLK_HIP_TRY(hipMemcpyAsync(pil + p.first, &p.second, sizeof(Fr), hipMemcpyHostToDevice, s));
+    // pin_small: [0, #pi) PI values uploaded here, [#pi, #pi + 16) the evaluations read
+    // back in round 4 (sized once: queued copies keep pointing into it)
+    TRY(key->pin_small.alloc((pis.size() + 16) * sizeof(Fr)));
+    for (size_t i = 0; i < pis.size(); ++i) {
+      key->pin_small.as<Fr>()[i] = pis[i].second;
+      PLK_HIP_TRY(hipMemcpyAsync(pil + pis[i].first, key->pin_small.as<Fr>() + i, sizeof(Fr),
+                                 hipMemcpyHostToDevice, s));
+    }
     TRY(ntt_run(key->dom, pil, key->pi_coef.as<Fr>(), n, -1, 0, nullptr, s, 1));
     Fr* ev = key->ev8.as<Fr>();  // z, a, b, c, d, pi, l1*alpha^2 over the 8n coset
     TRY(ntt_run(key->dom8, zc, ev + 0 * n8, n + 3, 1, 1, nullptr, s, 1));
@@ -807,8 +857,10 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     }
     TRY(pk_eval(eb, 16, n8, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
     Fr evs[16];
-    PLK_HIP_TRY(hipMemcpyAsync(evs, key->eval_out.ptr, sizeof evs, hipMemcpyDeviceToHost, s));
-    PLK_HIP_TRY(hipStreamSynchronize(s));
+    Fr* evs_pin = key->pin_small.as<Fr>() + pis.size();
+    PLK_HIP_TRY(hipMemcpyAsync(evs_pin, key->eval_out.ptr, sizeof evs, hipMemcpyDeviceToHost, s));
+    PLK_HIP_TRY(stream_wait(s));
+    std::memcpy(evs, evs_pin, sizeof evs);
     const Fr t_eval = evs[0], a_e = evs[1], b_e = evs[2], c_e = evs[3], d_e = evs[4];
     const Fr s1_e = evs[5], s2_e = evs[6], s3_e = evs[7];
     const Fr qar_e = evs[8], qc_e = evs[9], ql_e = evs[10], qr_e = evs[11];

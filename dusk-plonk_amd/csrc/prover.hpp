@@ -119,6 +119,7 @@ struct plk_key {
   plk::Fr vh_inv[8];
   plk_g1 comms[15];         // q_m q_l q_r q_o q_c q_4 q_arith q_range q_logic q_fixed q_var s1..s4
   // per-proof scratch
+  plk::PinnedBuf pin_witness, pin_small;  // host staging of the witness upload / small readbacks
   plk::DevBuf witness, wires_lag, wires_coef, z_lag, z_coef, num, den, tmp_a, tmp_b, scan_tmp,
       pi_lag, pi_coef, ev8, quot8, t_coef, r_coef, agg, agg2, w_coef, eval_partial, eval_out;
 };

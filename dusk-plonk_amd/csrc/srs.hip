@@ -127,7 +127,7 @@ int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   hipLaunchKernelGGL(k_table_to_rx, dim3(cdiv((uint64_t)s->windows * n, 256)), dim3(256), 0, stream,
                      tab, (uint64_t)s->windows * n);
   PLK_HIP_TRY(hipGetLastError());
-  PLK_HIP_TRY(hipStreamSynchronize(stream));
+  PLK_HIP_TRY(stream_wait(stream));
   s->ws.reset(new MsmWorkspace());
   return ws_reserve(s, n, 1);
 }
@@ -158,7 +158,7 @@ int srs_generate(plk_srs* s, const Fr& tau_mont, uint64_t start, hipStream_t str
                      temp.as<G1xyzz>(), (uint64_t)n, pref.as<Fp>(), s->points.as<G1Affine>(),
                      s->inf.as<uint8_t>());
   PLK_HIP_TRY(hipGetLastError());
-  PLK_HIP_TRY(hipStreamSynchronize(stream));
+  PLK_HIP_TRY(stream_wait(stream));
   return PLK_OK;
 }
 

@@ -1,0 +1,167 @@
+// ubench_acc.hip — variants of the MSM accumulation loop (msm.hip k_accumulate) on a
+// synthetic workload of the bench's shape: a 16M-entry affine table (R' domain values,
+// random coordinates: the instruction stream is the same as for curve points), tasks of
+// CH consecutive sorted entries with random table indices. Reports point adds/s for
+//   v0: the production loop (index load -> point load -> madd)
+//   v1: software-pipelined: the next index and point are loaded before the current madd
+//   v2: v0 with a 3-waves/SIMD register budget
+//   v3: v1 with a 3-waves/SIMD register budget
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/ubench_acc.hip -o tools/ubench_acc
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../dusk-plonk_amd/csrc/g1r.hpp"
+
+using namespace plk;
+
+#define CHECK(x)                                                                    \
+  do {                                                                              \
+    hipError_t e = (x);                                                             \
+    if (e != hipSuccess) {                                                          \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      return 1;                                                                     \
+    }                                                                               \
+  } while (0)
+
+__device__ __forceinline__ void ld_fp(const uint32_t* p, Fp& r) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint4 a = q[i];
+    r.v[4 * i] = a.x;
+    r.v[4 * i + 1] = a.y;
+    r.v[4 * i + 2] = a.z;
+    r.v[4 * i + 3] = a.w;
+  }
+}
+
+__device__ __forceinline__ void acc_plain(const uint2 task, const uint32_t* __restrict__ sorted,
+                                          const G1Affine* __restrict__ table, G1xyzz* out) {
+  G1R acc = g1r_infinity();
+  for (uint32_t e = task.x; e < task.x + task.y; ++e) {
+    const uint32_t code = sorted[e];
+    RFp x, y;
+    ld_g1r_aff(&table[code & 0x7fffffffu], x, y);
+    if (code & 0x80000000u) y = rx_neg(y);
+    acc = g1r_add_affine(acc, x, y);
+  }
+  st_g1r(out, acc);
+}
+
+__device__ __forceinline__ void acc_pipe(const uint2 task, const uint32_t* __restrict__ sorted,
+                                         const G1Affine* __restrict__ table, G1xyzz* out) {
+  G1R acc = g1r_infinity();
+  const uint32_t end = task.x + task.y;
+  uint32_t code = sorted[task.x];
+  Fp px, py;
+  {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(&table[code & 0x7fffffffu]);
+    ld_fp(q, px);
+    ld_fp(q + 12, py);
+  }
+  for (uint32_t e = task.x; e < end; ++e) {
+    RFp x = rx_unpack(px), y = rx_unpack(py);
+    if (code & 0x80000000u) y = rx_neg(y);
+    if (e + 1 < end) {  // issue the next loads before the madd
+      code = sorted[e + 1];
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(&table[code & 0x7fffffffu]);
+      ld_fp(q, px);
+      ld_fp(q + 12, py);
+    }
+    acc = g1r_add_affine(acc, x, y);
+  }
+  st_g1r(out, acc);
+}
+
+__global__ void __launch_bounds__(256) k_v0(const uint2* tasks, uint32_t ntasks,
+                                            const uint32_t* sorted, const G1Affine* table,
+                                            G1xyzz* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ntasks) acc_plain(tasks[t], sorted, table, &out[t]);
+}
+__global__ void __launch_bounds__(256) k_v1(const uint2* tasks, uint32_t ntasks,
+                                            const uint32_t* sorted, const G1Affine* table,
+                                            G1xyzz* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ntasks) acc_pipe(tasks[t], sorted, table, &out[t]);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+k_v2(const uint2* tasks, uint32_t ntasks, const uint32_t* sorted, const G1Affine* table,
+     G1xyzz* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ntasks) acc_plain(tasks[t], sorted, table, &out[t]);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+k_v3(const uint2* tasks, uint32_t ntasks, const uint32_t* sorted, const G1Affine* table,
+     G1xyzz* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ntasks) acc_pipe(tasks[t], sorted, table, &out[t]);
+}
+
+static uint64_t g_s = 0x9e37;
+static uint32_t rnd() {
+  g_s += 0x9E3779B97F4A7C15ull;
+  uint64_t z = g_s;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)(z ^ (z >> 31));
+}
+
+int main() {
+  const uint32_t npts = 16u << 20;   // 2^20 points x 16 windows
+  const uint32_t entries = 16u << 20;  // one MSM of 2^20 scalars x 16 windows
+  const uint32_t CH = 32, ntasks = entries / CH;
+  std::vector<G1Affine> tab(npts);
+  for (auto& p : tab) {
+    for (int k = 0; k < 12; ++k) {
+      p.x.v[k] = rnd();
+      p.y.v[k] = rnd();
+    }
+    p.x.v[11] &= 0x0fffffffu;  // < p
+    p.y.v[11] &= 0x0fffffffu;
+  }
+  std::vector<uint32_t> sorted(entries);
+  for (auto& s : sorted) s = (rnd() % npts) | (rnd() & 0x80000000u);
+  std::vector<uint2> tasks(ntasks);
+  for (uint32_t t = 0; t < ntasks; ++t) tasks[t] = make_uint2(t * CH, CH);
+  G1Affine* dtab;
+  uint32_t* dsorted;
+  uint2* dtasks;
+  G1xyzz* dout;
+  CHECK(hipMalloc(&dtab, (size_t)npts * sizeof(G1Affine)));
+  CHECK(hipMalloc(&dsorted, (size_t)entries * 4));
+  CHECK(hipMalloc(&dtasks, (size_t)ntasks * 8));
+  CHECK(hipMalloc(&dout, (size_t)ntasks * sizeof(G1xyzz)));
+  CHECK(hipMemcpy(dtab, tab.data(), (size_t)npts * sizeof(G1Affine), hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(dsorted, sorted.data(), (size_t)entries * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(dtasks, tasks.data(), (size_t)ntasks * 8, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  void (*ks[4])(const uint2*, uint32_t, const uint32_t*, const G1Affine*, G1xyzz*) = {k_v0, k_v1, k_v2, k_v3};
+  const char* names[4] = {"v0_plain", "v1_pipelined", "v2_plain_w3", "v3_pipelined_w3"};
+  std::vector<G1xyzz> ref(ntasks), got(ntasks);
+  for (int v = 0; v < 4; ++v) {
+    const dim3 grid((ntasks + 255) / 256);
+    hipLaunchKernelGGL(ks[v], grid, dim3(256), 0, 0, dtasks, ntasks, dsorted, dtab, dout);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    const int reps = 3;
+    for (int r = 0; r < reps; ++r)
+      hipLaunchKernelGGL(ks[v], grid, dim3(256), 0, 0, dtasks, ntasks, dsorted, dtab, dout);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipMemcpy(v == 0 ? ref.data() : got.data(), dout, (size_t)ntasks * sizeof(G1xyzz),
+                    hipMemcpyDeviceToHost));
+    bool same = true;
+    if (v) same = memcmp(ref.data(), got.data(), (size_t)ntasks * sizeof(G1xyzz)) == 0;
+    std::printf("{\"test\":\"%s\",\"ms_per_msm\":%.3f,\"adds_per_s\":%.4e,\"same_as_v0\":%s}\n",
+                names[v], ms / reps, (double)entries * reps / (ms * 1e-3), same ? "true" : "false");
+  }
+  return 0;
+}
