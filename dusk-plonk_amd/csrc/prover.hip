@@ -527,6 +527,36 @@ int plk_composer_public_inputs(const plk_composer* c, plk_fr* values, uint64_t* 
   return PLK_OK;
 }
 
+int plk_composer_export(const plk_composer* c, plk_constraint* gates, size_t cap,
+                        plk_fr* witness, size_t wcap, size_t* m, size_t* nw) {
+  if (!c) return PLK_E_ARG;
+  if (m) *m = c->gates.size();
+  if (nw) *nw = c->witness.size();
+  if (gates) {
+    const size_t cnt = std::min(cap, c->gates.size());
+    for (size_t i = 0; i < cnt; ++i) {
+      const Gate g = gate_unpack(c, i);
+      plk_constraint& o = gates[i];
+      plk_fr* qs[11] = {&o.q_m,     &o.q_l,   &o.q_r,     &o.q_o,
+                        &o.q_4,     &o.q_c,   &o.q_arith, &o.q_range,
+                        &o.q_logic, &o.q_fixed_group_add, &o.q_variable_group_add};
+      for (int q = 0; q < 11; ++q) *qs[q] = fr_to(g.q[q]);
+      o.a = g.w[0];
+      o.b = g.w[1];
+      o.o = g.w[2];
+      o.d = g.w[3];
+      o.has_public = g.has_pi ? 1u : 0u;
+      o._pad = 0;
+      o.public_input = fr_to(g.pi);
+    }
+  }
+  if (witness) {
+    const size_t cnt = std::min(wcap, c->witness.size());
+    for (size_t j = 0; j < cnt; ++j) witness[j] = fr_to(c->witness[j]);
+  }
+  return PLK_OK;
+}
+
 // ---------------------------------------------------------------------------- key
 int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk_key** out) {
   try {

@@ -71,6 +71,7 @@ def _bind():
         "plk_composer_component_boolean": [vp, u32],
         "plk_composer_synthetic_chain": [vp, sz, u64],
         "plk_composer_public_inputs": [vp, vp, vp, sz, C.POINTER(sz)],
+        "plk_composer_export": [vp, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(sz)],
         "plk_key_compile": [vp, vp, C.c_char_p, pp], "plk_key_destroy": [vp],
         "plk_key_info": [vp, C.POINTER(u64), C.POINTER(u64), vp],
         "plk_prove": [vp, vp, u64, vp, vp, sz, C.POINTER(sz)],
@@ -228,6 +229,19 @@ class Plonk:
 
     def synthetic_chain(self, gates: int, seed: int):
         _check(_bind().plk_composer_synthetic_chain(self._h, gates, seed), "synthetic_chain")
+
+    def export(self):
+        """(gates, witness): the circuit as uint64 arrays — gates (m, 51) in plk_constraint
+        layout, witness (nw, 4) Montgomery Fr (plk_composer_export)."""
+        lib = _bind()
+        m, nw = C.c_size_t(), C.c_size_t()
+        _check(lib.plk_composer_export(self._h, None, 0, None, 0, C.byref(m), C.byref(nw)),
+               "export")
+        gates = np.zeros((max(1, m.value), C.sizeof(PlkConstraint) // 8), dtype=np.uint64)
+        wit = np.zeros((max(1, nw.value), 4), dtype=np.uint64)
+        _check(lib.plk_composer_export(self._h, _ptr(gates), m.value, _ptr(wit), nw.value,
+                                       C.byref(m), C.byref(nw)), "export")
+        return gates[: m.value], wit[: nw.value]
 
     def public_inputs(self):
         cnt = C.c_size_t()

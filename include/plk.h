@@ -191,6 +191,11 @@ int plk_composer_synthetic_chain(plk_composer* c, size_t gates, uint64_t seed);
 /* Plonk::instance(): public inputs sorted by gate index, and their indexes. */
 int plk_composer_public_inputs(const plk_composer* c, plk_fr* values, uint64_t* indexes,
                                size_t cap, size_t* count);
+/* The circuit as the composer holds it (Plonk::constraints and the witness vector,
+ * lib.rs:103-115): gates[i] for i < min(cap, m) and witness[j] for j < min(wcap, #witness);
+ * *m / *nw receive the full sizes. For external checkers and serialisation. */
+int plk_composer_export(const plk_composer* c, plk_constraint* gates, size_t cap,
+                        plk_fr* witness, size_t wcap, size_t* m, size_t* nw);
 
 /* PlonkKey::compile_with_circuit (src/key.rs:63-327): device-resident proving key for the
  * circuit's structure, committed against `srs` (trimmed to next_pow2(m + 6) + 8 points).

@@ -1,4 +1,5 @@
-"""ctypes binding of the C oracle (oracle/plk_oracle.c) — test infrastructure only."""
+"""ctypes binding of the C oracle (oracle/plk_oracle.c, oracle/plk_prover_oracle.c) — test
+infrastructure only."""
 from __future__ import annotations
 
 import ctypes as C
@@ -22,6 +23,9 @@ class Oracle:
             "orc_elements": (None, [u32, vp, i32]), "orc_ntt": (i32, [vp, u32, i32, i32, i32]),
             "orc_vanishing": (None, [u32, u64, vp]), "orc_msm": (i32, [vp, vp, sz, vp, i32]),
             "orc_g1_mul": (None, [vp, vp, vp]), "orc_srs": (None, [vp, sz, vp, i32]),
+            "orc_merlin_test": (None, [vp]),
+            "orc_prove": (i32, [vp, sz, vp, sz, vp, sz, C.c_char_p, u64, i32, vp, vp, vp, vp,
+                                vp, sz, C.POINTER(sz), vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -75,6 +79,38 @@ class Oracle:
         self.lib.orc_srs(self._p(t), n, self._p(out), threads)
         return out
 
+    def merlin_test(self) -> bytes:
+        out = (C.c_uint8 * 32)()
+        self.lib.orc_merlin_test(out)
+        return bytes(out)
+
+    def prove(self, gates: np.ndarray, witness: np.ndarray, srs: np.ndarray, label: bytes,
+              seed: int, threads: int = 0, vk_in=None):
+        """orc_prove: restated PlonkKey::compile + create_proof. gates: (m, 51) u64 words in
+        plk_constraint layout; witness (nw, 4); srs (N, 13). Returns dict with vk (15, 13),
+        comms (11, 13), evals (16, 4), pis (k, 4), timing_ns (8,)."""
+        g = np.ascontiguousarray(gates, dtype=np.uint64)
+        w = np.ascontiguousarray(witness, dtype=np.uint64).reshape(-1, 4)
+        pts = np.ascontiguousarray(srs, dtype=np.uint64).reshape(-1, 13)
+        vk = np.zeros((15, 13), dtype=np.uint64)
+        comms = np.zeros((11, 13), dtype=np.uint64)
+        evals = np.zeros((16, 4), dtype=np.uint64)
+        pis = np.zeros((max(1, g.shape[0]), 4), dtype=np.uint64)
+        npi = C.c_size_t()
+        timing = np.zeros(8, dtype=np.uint64)
+        vin = None
+        if vk_in is not None:
+            vin = np.ascontiguousarray(vk_in, dtype=np.uint64).reshape(15, 13)
+        st = self.lib.orc_prove(self._p(g), g.shape[0], self._p(w), w.shape[0], self._p(pts),
+                                pts.shape[0], label, seed, threads,
+                                None if vin is None else self._p(vin), self._p(vk),
+                                self._p(comms), self._p(evals), self._p(pis), pis.shape[0],
+                                C.byref(npi), self._p(timing))
+        if st != 0:
+            raise RuntimeError(f"orc_prove status {st}")
+        return {"vk": vk, "comms": comms, "evals": evals, "pis": pis[: npi.value],
+                "timing_ns": timing}
+
     def fr_mul(self, a, b):
         a = np.ascontiguousarray(a, dtype=np.uint64)
         b = np.ascontiguousarray(b, dtype=np.uint64)
@@ -84,8 +120,8 @@ class Oracle:
 
 
 def load() -> Oracle:
-    src = ORACLE_DIR / "plk_oracle.c"
-    if not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
+    srcs = [ORACLE_DIR / "plk_oracle.c", ORACLE_DIR / "plk_prover_oracle.c"]
+    if not LIB.exists() or any(LIB.stat().st_mtime < s.stat().st_mtime for s in srcs):
         subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
     return Oracle(C.CDLL(str(LIB)))
 
