@@ -215,6 +215,57 @@ def cpu_baseline(k: int, pp, threads: int):
     }
 
 
+def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
+    """Restated reference CPU prover (oracle/plk_prover_oracle.c: key compile + create_proof
+    in the reference's order and cost structure, OpenMP where the reference uses rayon,
+    sequential where it is sequential — notably the quotient loop's one v_h inversion per
+    8n point, quotient_poly.rs:99-107). One full CPU proof at 2^k_sample is timed by
+    phase; its O(n) phases scale by n / 2^k_sample, and the MSM and NTT phases are timed
+    directly at the 2^k sizes (11 MSM(n), 11 NTT(n), 8 NTT(8n) per proof)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    from dusk_plonk_amd.prover import Plonk
+    orc = oracle_lib.load()
+    ks = min(k, k_sample)
+    n, ns = 1 << k, 1 << ks
+    cs = Plonk()
+    cs.synthetic_chain(ns - 14, 77)
+    gates, wit = cs.export()
+    trim = (1 << (gates.shape[0] + 6 - 1).bit_length()) + 8
+    res = orc.prove(gates, wit, pp.points(0, trim), b"cpu-baseline", 5, threads)
+    tm = res["timing_ns"].astype(np.float64) / 1e9
+    prove_s, msm_s, ntt_s = tm[6], tm[1], tm[2]
+    other_s = prove_s - msm_s - ntt_s  # quotient loop, grand product, openings, transcript
+    if ks == k:
+        t_msm = msm_s / 11
+        per_proof = prove_s
+        t_ntt = t_ntt8 = float("nan")
+    else:
+        pts = pp.points(0, n)
+        sc = oracle_lib.random_fr(n, 77)
+        v8 = oracle_lib.random_fr(8 * n, 78)
+        t0 = time.perf_counter()
+        orc.msm(pts, sc, threads)
+        t_msm = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        orc.dft(sc, k, threads)
+        t_ntt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        orc.coset_dft(v8, k + 3, threads)
+        t_ntt8 = time.perf_counter() - t0
+        per_proof = 11 * t_msm + 11 * t_ntt + 8 * t_ntt8 + other_s * (n / ns)
+    return {
+        "value": n / per_proof, "unit": "constraints/s", "cores": threads, "kind": "port",
+        "sample": (f"oracle/plk_prover_oracle.c (restated reference CPU prover, OpenMP {threads} "
+                   f"threads): one full create_proof at 2^{ks} = {prove_s:.2f} s "
+                   f"({ns / prove_s:.0f} constraints/s; MSM {msm_s:.2f} s, NTT {ntt_s:.2f} s, "
+                   f"quotient loop {tm[3]:.2f} s, grand product {tm[4]:.2f} s, openings "
+                   f"{tm[5]:.2f} s); per proof at 2^{k} = 11 x MSM(2^{k}) {t_msm:.2f} s + "
+                   f"11 x dft(2^{k}) {t_ntt:.3f} s + 8 x coset_dft(2^{k + 3}) {t_ntt8:.3f} s + "
+                   f"O(n) phases x {n // ns} = {per_proof:.1f} s"),
+    }
+
+
 def load_pmc_traffic(kernel_substr: str):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary."""
     f = ROOT / "profiles" / "pmc_traffic.json"
@@ -289,7 +340,7 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(k, fp.pp, threads)
+        result["cpu_baseline"] = cpu_baseline_full(k, fp.pp, threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

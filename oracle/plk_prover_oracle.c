@@ -328,8 +328,8 @@ static void ntt_timed(uint64_t* data, uint32_t log_n, int dir, int coset, int th
  * instead of committing the selectors and sigmas (the CPU-baseline timing mode).
  * Outputs: vk (15 x 13 words), proof commitments (11 x 13), evaluations (16 x 4 words,
  * plk_proof order), public inputs (count written to *pi_count, up to pi_cap values), and
- * timing[8] in ns: {compile, msm, ntt, quotient loop, grand product, widget+lin+openings
- * other, prove total, transcript}.
+ * timing[8] in ns: {key compile, proof MSMs, proof NTTs, quotient loop, grand product,
+ * linearisation + openings, create_proof total, transcript}.
  */
 int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t nw,
               const uint64_t* srs, size_t srs_len, const char* label, uint64_t seed,
@@ -448,6 +448,7 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   /* ==================================================================== create_proof */
   const uint64_t t_prove = now_ns();
   uint64_t t_tr = 0, t0;
+  tm[1] = tm[2] = 0; /* from here on the MSM / NTT timers cover create_proof only */
   orc_rng rng = {seed};
   orc_transcript tr;
   t0 = now_ns();
