@@ -266,8 +266,10 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
     }
 
 
-def load_pmc_traffic(kernel_substr: str):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary."""
+def load_pmc_traffic(kernel_substr: str, key: str = "hbm_bytes_per_launch"):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, made by tools/gpu_pmc.sh + tools/pmc_summary.py from the
+    default bench command). key "hbm_bytes_last_launch" = the run's last dispatch."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None
@@ -275,7 +277,7 @@ def load_pmc_traffic(kernel_substr: str):
         d = json.loads(f.read_text())
         for name, rec in d.get("kernels", {}).items():
             if kernel_substr in name:
-                return rec.get("hbm_bytes_per_launch")
+                return rec.get(key, rec.get("hbm_bytes_per_launch"))
     except Exception:
         return None
     return None
@@ -333,7 +335,7 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
         result["roofline"] = {
             "bound": "hbm", "kernel": "k_accumulate", "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": load_pmc_traffic("k_accumulate"),
+            "traffic": load_pmc_traffic("k_accumulate", "hbm_bytes_last_launch"),
             "algorithmic_bytes_per_launch": 128.0 * n * 2, "avg_launch_ms": ms,
             "point_adds_per_launch": adds, "point_adds_per_s": adds / (ms * 1e-3),
             "note": "integer-VALU-bound (no MFMA); HBM reported as the required secondary roofline",

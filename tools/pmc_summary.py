@@ -22,6 +22,7 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     for k, v in vals.items():
         per[k][counter] = sum(v) / len(v)
+        per[k][counter + "_last"] = v[-1]
         per[k]["launches"] = len(v)
 kernels = {}
 for k, d in per.items():
@@ -30,6 +31,9 @@ for k, d in per.items():
         "launches": d["launches"], "fetch_kb": fe, "write_kb": wr,
         "hbm_bytes_per_launch": (fe + wr) * 1024,
         "hbm_bytes_per_launch_stream_corrected": (2 * fe + wr) * 1024,
+        # the last dispatch of the run (bench.py: the proof's opening-commit batch, the
+        # launch its roofline `achieved` is computed for)
+        "hbm_bytes_last_launch": (d.get("FETCH_SIZE_last", 0.0) + d.get("WRITE_SIZE_last", 0.0)) * 1024,
     }
 json.dump({"source": str(src), "kernels": kernels}, open(out, "w"), indent=1, sort_keys=True)
 print(f"wrote {out} ({len(kernels)} kernels)")
