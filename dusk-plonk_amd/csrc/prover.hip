@@ -456,6 +456,50 @@ int plk_composer_assert_equal_constant(plk_composer* c, uint32_t a, const plk_fr
   return PLK_OK;
 }
 
+// component_range (lib.rs:1066-1163): base-4 accumulators over the witness's canonical bits
+// (LSB first), 4 quads per width-4 gate with q_range = 1 (d, o, b, a order within a gate,
+// the next gate's d closing the chain), a final zero-selector gate carrying the last
+// accumulator, and the last accumulator asserted equal to the witness.
+int plk_composer_component_range(plk_composer* c, uint32_t witness, size_t num_bits) {
+  if (!c || witness >= c->witness.size() || num_bits > 256) return PLK_E_ARG;
+  try {
+    const Fr canon = fe_from_mont(c->witness[witness]);
+    auto bit = [&](size_t i) -> uint32_t { return (canon.v[i / 32] >> (i % 32)) & 1u; };
+    size_t num_gates = num_bits >> 3;
+    if (num_bits % 8 != 0) ++num_gates;
+    const size_t num_quads = num_gates * 4;
+    const size_t pad = 1 + (((num_quads << 1) - num_bits) >> 1);
+    Gate base = default_gate();
+    base.q[QRANGE] = fe_one<FrCfg>();  // Constraint::range
+    std::vector<Gate> cons(num_gates + 1, base);
+    std::vector<uint32_t> accs;
+    const Fr four = fr_u64(4);
+    Fr acc = fe_zero<FrCfg>();
+    for (size_t i = pad; i <= num_quads; ++i) {
+      const size_t bi = (num_quads - i) << 1;
+      const uint32_t quad = (bi < 256 ? bit(bi) : 0u) + 2 * (bi + 1 < 256 ? bit(bi + 1) : 0u);
+      acc = fe_add(fe_mul(four, acc), fr_u64(quad));
+      const uint32_t w = append_witness(c, acc);
+      accs.push_back(w);
+      Gate& g = cons[i / 4];
+      switch (i % 4) {
+        case 0: g.w[3] = w; break;
+        case 1: g.w[2] = w; break;
+        case 2: g.w[1] = w; break;
+        default: g.w[0] = w; break;
+      }
+    }
+    cons.back() = default_gate();
+    if (!accs.empty()) cons.back().w[3] = accs.back();
+    for (const Gate& g : cons)
+      if (append_custom_gate(c, g) != PLK_OK) return PLK_E_ARG;
+    if (!accs.empty()) return plk_composer_assert_equal(c, accs.back(), witness);
+    return PLK_OK;
+  } catch (...) {
+    return PLK_E_OOM;
+  }
+}
+
 int plk_composer_component_boolean(plk_composer* c, uint32_t a) {
   if (!c || a >= c->witness.size()) return PLK_E_ARG;
   Gate g = default_gate();  // lib.rs:859-872

@@ -45,7 +45,8 @@ ABI_SYMBOLS = (
     "plk_composer_append_witness", "plk_composer_witness_value", "plk_composer_set_witness",
     "plk_composer_append_public", "plk_composer_append_gate", "plk_composer_append_custom_gate",
     "plk_composer_gate_eval", "plk_composer_assert_equal", "plk_composer_assert_equal_constant",
-    "plk_composer_component_boolean", "plk_composer_synthetic_chain",
+    "plk_composer_component_boolean", "plk_composer_component_range",
+    "plk_composer_synthetic_chain",
     "plk_composer_public_inputs", "plk_composer_export", "plk_key_compile", "plk_key_destroy",
     "plk_key_info",
     "plk_prove",

@@ -69,6 +69,7 @@ def _bind():
         "plk_composer_assert_equal": [vp, u32, u32],
         "plk_composer_assert_equal_constant": [vp, u32, vp, vp],
         "plk_composer_component_boolean": [vp, u32],
+        "plk_composer_component_range": [vp, u32, sz],
         "plk_composer_synthetic_chain": [vp, sz, u64],
         "plk_composer_public_inputs": [vp, vp, vp, sz, C.POINTER(sz)],
         "plk_composer_export": [vp, vp, sz, vp, sz, C.POINTER(sz), C.POINTER(sz)],
@@ -226,6 +227,9 @@ class Plonk:
 
     def component_boolean(self, a: int):
         _check(_bind().plk_composer_component_boolean(self._h, a), "component_boolean")
+
+    def component_range(self, a: int, num_bits: int):
+        _check(_bind().plk_composer_component_range(self._h, a, num_bits), "component_range")
 
     def synthetic_chain(self, gates: int, seed: int):
         _check(_bind().plk_composer_synthetic_chain(self._h, gates, seed), "synthetic_chain")

@@ -186,6 +186,9 @@ int plk_composer_assert_equal(plk_composer* c, uint32_t a, uint32_t b);         
 int plk_composer_assert_equal_constant(plk_composer* c, uint32_t a, const plk_fr* constant,
                                        const plk_fr* public_input /* nullable */);  /* :766 */
 int plk_composer_component_boolean(plk_composer* c, uint32_t a);                   /* :859 */
+/* component_range (lib.rs:1066-1163): constrain `a` to num_bits (<= 256) bits with the
+ * range widget; an out-of-range value makes create_proof fail (tests/range.rs:82-84). */
+int plk_composer_component_range(plk_composer* c, uint32_t a, size_t num_bits);
 /* The bench circuit: `gates` chained gates x' = x*y + x (q_m = q_l = 1, q_o = -1). */
 int plk_composer_synthetic_chain(plk_composer* c, size_t gates, uint64_t seed);
 /* Plonk::instance(): public inputs sorted by gate index, and their indexes. */

@@ -52,6 +52,31 @@ class Chain:
         cs.synthetic_chain(self.gates, self.seed)
 
 
+class Ranged:
+    """tests/range.rs:27-55 DummyCircuit: component_range(a, bits)."""
+
+    def __init__(self, a, bits):
+        self.a, self.bits = a, bits
+
+    def synthesize(self, cs):
+        cs.component_range(cs.append_witness(self.a), self.bits)
+
+
+def test_range_works(plk):
+    """tests/range.rs:14-99: compile with the default circuit (7, 76 bits), prove u64::MAX,
+    reject -2^77, and compile with 77 bits."""
+    from dusk_plonk_amd.prover import PlonkKey
+    r = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    tau, pp = tau_and_params(plk, 6, 8349)
+    prover, vd = PlonkKey.compile_with_circuit(pp, b"demo", Ranged(7, 76))
+    proof, pi = prover.create_proof(1, Ranged(2**64 - 1, 76))
+    verify(vd, proof, pi, tau)
+    with pytest.raises(plk.PlonkError) as e:
+        prover.create_proof(2, Ranged((r - 2**77) % r, 76))
+    assert e.value.status == plk.PLK_E_DEGREE
+    PlonkKey.compile_with_circuit(pp, b"demo", Ranged(1, 77))
+
+
 def test_boolean_works(plk):
     from dusk_plonk_amd.prover import PlonkKey
     tau, pp = tau_and_params(plk, 4, 8349)

@@ -78,7 +78,20 @@ def public_and_chain(gates, seed, pub):
     return f
 
 
+def ranged(a, bits):
+    """tests/range.rs DummyCircuit: component_range(append_witness(a), bits)."""
+    def f(cs):
+        cs.component_range(cs.append_witness(a), bits)
+    return f
+
+
+R_MOD = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
 CASES = [
+    ("range_u64max_76", ranged(2**64 - 1, 76), 31),
+    ("range_7_76", ranged(7, 76), 32),
+    ("range_odd_77", ranged(1, 77), 33),
+    ("range_full_254", ranged(2**250 + 12345, 254), 34),
     ("boolean1", boolean(1), 11),
     ("boolean0", boolean(0), 12),
     ("public_sum", public_sum(10, 20, 30), 5),
@@ -118,9 +131,11 @@ def test_oracle_proof_verifies(plk, oracle, name, fn, seed):
         verify(vd, proof, pis, tau)
 
 
-def test_oracle_rejects_unsatisfied(plk, oracle):
+@pytest.mark.parametrize("fn", [boolean(2), ranged((R_MOD - 2**77) % R_MOD, 76),
+                                ranged(2**76, 76)], ids=["boolean2", "range_neg", "range_2^76"])
+def test_oracle_rejects_unsatisfied(plk, oracle, fn):
     tau_limbs, _ = tau_for(1)
-    cs = build(boolean(2))
+    cs = build(fn)
     with pytest.raises(RuntimeError, match="status 2"):  # ORC_E_DEGREE at the t commit
         oracle_prove(oracle, cs, b"oracle", 1, tau_limbs)
 
