@@ -625,9 +625,10 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     if (k + 3 > 27) return PLK_E_ARG;
     for (uint64_t i = 0; i < m; ++i) {
       const Gate g = gate_unpack(cs, i);
-      if (!fe_is_zero(g.q[QLOGIC]) || !fe_is_zero(g.q[QFIXED]) || !fe_is_zero(g.q[QVAR]))
-        return PLK_E_UNSUPPORTED;  // logic / curve widgets: next round
+      if (!fe_is_zero(g.q[QFIXED]) || !fe_is_zero(g.q[QVAR]))
+        return PLK_E_UNSUPPORTED;  // curve widgets: next round
       if (!fe_is_zero(g.q[QRANGE])) key->has_range = true;
+      if (!fe_is_zero(g.q[QLOGIC])) key->has_logic = true;
     }
     TRY(plk_domain_get(ctx, k, &key->dom));
     TRY(plk_domain_get(ctx, k + 3, &key->dom8));
@@ -691,7 +692,7 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
 
     // 4. 8n coset evaluations (key.rs:220-245) and v_h over the coset (key.rs:291)
     TRY(key->sel8.alloc(SEL_COUNT8 * n8 * sizeof(Fr)));
-    const int sel_src[SEL_COUNT8] = {QM, QL, QR, QO, Q4, QC, QARITH, QRANGE};
+    const int sel_src[SEL_COUNT8] = {QM, QL, QR, QO, Q4, QC, QARITH, QRANGE, QLOGIC};
     for (int j = 0; j < SEL_COUNT8; ++j)
       TRY(ntt_run(key->dom8, qc + sel_src[j] * n, key->sel8.as<Fr>() + j * n8, n, 1, 1, nullptr, s, 1));
     TRY(key->sigma8.alloc(4 * n8 * sizeof(Fr)));
@@ -854,7 +855,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     // ---- round 3: quotient (prover.rs:201-287, quotient_poly.rs)
     const Fr alpha = tr.challenge_scalar("alpha");
     const Fr range_sep = tr.challenge_scalar("range separation challenge");
-    (void)tr.challenge_scalar("logic separation challenge");
+    const Fr logic_sep = tr.challenge_scalar("logic separation challenge");
     (void)tr.challenge_scalar("fixed base separation challenge");
     (void)tr.challenge_scalar("variable base separation challenge");
     Fr* pil = key->pi_lag.as<Fr>();
@@ -901,6 +902,12 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     qa.kappa2 = fe_sqr(qa.kappa);
     qa.kappa3 = fe_mul(qa.kappa2, qa.kappa);
     qa.has_range = key->has_range ? 1 : 0;
+    qa.logic_sep = logic_sep;
+    qa.lk = fe_sqr(logic_sep);
+    qa.lk2 = fe_sqr(qa.lk);
+    qa.lk3 = fe_mul(qa.lk2, qa.lk);
+    qa.lk4 = fe_mul(qa.lk3, qa.lk);
+    qa.has_logic = key->has_logic ? 1 : 0;
     for (int j = 0; j < 8; ++j) qa.vh_inv[j] = key->vh_inv[j];
     TRY(pk_quotient(qa, s));
     Fr* tc = key->t_coef.as<Fr>();
@@ -965,8 +972,21 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       r = fe_add(r, fe_mul(delta(fe_sub(dn_e, four(a_e))), qa.kappa3));
       term(qc + QRANGE * n, n, fe_mul(r, range_sep));
     }
-    (void)an_e;
-    (void)bn_e;
+    if (key->has_logic) {  // logic::linearize: q_logic(X) * sep * (...) at the evaluations
+      const Fr two = fe_dbl(one), three = fe_add(two, one), four = fe_dbl(two);
+      auto delta = [&](const Fr& f) {
+        return fe_mul(fe_mul(f, fe_sub(f, one)), fe_mul(fe_sub(f, two), fe_sub(f, three)));
+      };
+      const Fr qa_ = fe_sub(an_e, fe_mul(four, a_e));
+      const Fr qb_ = fe_sub(bn_e, fe_mul(four, b_e));
+      const Fr qd_ = fe_sub(dn_e, fe_mul(four, d_e));
+      Fr r = delta(qa_);
+      r = fe_add(r, fe_mul(delta(qb_), qa.lk));
+      r = fe_add(r, fe_mul(delta(qd_), qa.lk2));
+      r = fe_add(r, fe_mul(fe_sub(c_e, fe_mul(qa_, qb_)), qa.lk3));
+      r = fe_add(r, fe_mul(logic_xor_and(qa_, qb_, c_e, qd_, qc_e), qa.lk4));
+      term(qc + QLOGIC * n, n, fe_mul(r, logic_sep));
+    }
     // z(X) * [(a + b z + g)(b + b K1 z + g)(c + b K2 z + g)(d + b K3 z + g) alpha + L1(z) alpha^2]
     const Fr bz = fe_mul(beta, zeta);
     Fr idc = fe_mul(fe_add(fe_add(a_e, bz), gamma), fe_add(fe_add(b_e, fe_mul(K1, bz)), gamma));

@@ -17,7 +17,8 @@ struct BlindArgs {
 };
 
 // selector rows of the 8n evaluation table
-enum { SEL_QM = 0, SEL_QL, SEL_QR, SEL_QO, SEL_Q4, SEL_QC, SEL_QARITH, SEL_QRANGE, SEL_COUNT8 };
+enum { SEL_QM = 0, SEL_QL, SEL_QR, SEL_QO, SEL_Q4, SEL_QC, SEL_QARITH, SEL_QRANGE, SEL_QLOGIC,
+       SEL_COUNT8 };
 
 struct QuotientArgs {
   const Fr *a, *b, *c, *d, *z, *pi, *l1a, *sel, *sigma, *elements8;
@@ -25,7 +26,8 @@ struct QuotientArgs {
   uint64_t n8;
   Fr g, alpha, beta, gamma, k1, k2, k3;
   Fr range_sep, kappa, kappa2, kappa3;
-  int has_range;
+  Fr logic_sep, lk, lk2, lk3, lk4;  // logic separation challenge and its kappa powers
+  int has_range, has_logic;
   Fr vh_inv[8];
 };
 
@@ -43,6 +45,28 @@ struct LinComb {
   Fr s[kMaxTerms];
   uint32_t terms;
 };
+
+// delta_xor_and: 3(a + b + c) - 2 f + q_c (9c - 3(a + b)) with
+// f = w (w (4w - 18(a + b) + 81) + 18(a^2 + b^2) - 81(a + b) + 83) = 6 (a AND b) for quads
+PLK_HD Fr logic_xor_and(const Fr& a, const Fr& b, const Fr& w, const Fr& c,
+                                            const Fr& qc) {
+  auto k = [](uint32_t v) {
+    Fr x = fe_zero<FrCfg>();
+    x.v[0] = v;
+    return fe_to_mont(x);
+  };
+  const Fr ab = fe_add(a, b);
+  Fr f = fe_sub(fe_mul(k(4), w), fe_mul(k(18), ab));
+  f = fe_add(f, k(81));
+  f = fe_mul(w, f);
+  f = fe_add(f, fe_mul(k(18), fe_add(fe_sqr(a), fe_sqr(b))));
+  f = fe_sub(f, fe_mul(k(81), ab));
+  f = fe_add(f, k(83));
+  f = fe_mul(w, f);
+  const Fr e = fe_sub(fe_mul(k(3), fe_add(ab, c)), fe_dbl(f));
+  const Fr bb = fe_mul(qc, fe_sub(fe_mul(k(9), c), fe_mul(k(3), ab)));
+  return fe_add(bb, e);
+}
 
 int pk_gather_wires(const Fr* witness, const uint32_t* idx, uint64_t m, uint64_t n, Fr* out,
                     hipStream_t s);
@@ -108,7 +132,7 @@ struct plk_key {
   uint32_t k = 0;
   plk_domain* dom = nullptr;   // n
   plk_domain* dom8 = nullptr;  // 8n
-  bool has_range = false;
+  bool has_range = false, has_logic = false;
   // device-resident proving key
   plk::DevBuf q_coef;       // 11 x n selector coefficient polys
   plk::DevBuf sel8;         // SEL_COUNT8 x 8n coset evaluations

@@ -215,6 +215,29 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
       t = fe_add(t, fe_mul(fe_mul(r, qr), q.range_sep));
     }
   }
+  // logic widget (dusk-plonk logic gate; zksnarks, un-vendored): quads a = a_next - 4a,
+  // b = b_next - 4b, d = d_next - 4d, w = c; sep q_logic (D(a) + D(b) k + D(d) k^2 +
+  // (w - ab) k^3 + xor_and(a, b, w, d, q_c) k^4), k = sep^2
+  if (q.has_logic) {
+    const Fr ql = ldf(&q.sel[SEL_QLOGIC * N + i]);
+    if (!fe_is_zero(ql)) {
+      const Fr one = fe_one<FrCfg>();
+      const Fr two = fe_dbl(one), three = fe_add(two, one), four = fe_dbl(two);
+      auto delta = [&](const Fr& f) {
+        return fe_mul(fe_mul(f, fe_sub(f, one)), fe_mul(fe_sub(f, two), fe_sub(f, three)));
+      };
+      const Fr qa = fe_sub(ldf(&q.a[nx]), fe_mul(four, a));
+      const Fr qb = fe_sub(ldf(&q.b[nx]), fe_mul(four, b));
+      const Fr qd = fe_sub(ldf(&q.d[nx]), fe_mul(four, d));
+      const Fr qc = ldf(&q.sel[SEL_QC * N + i]);
+      Fr r = delta(qa);
+      r = fe_add(r, fe_mul(delta(qb), q.lk));
+      r = fe_add(r, fe_mul(delta(qd), q.lk2));
+      r = fe_add(r, fe_mul(fe_sub(c, fe_mul(qa, qb)), q.lk3));
+      r = fe_add(r, fe_mul(logic_xor_and(qa, qb, c, qd, qc), q.lk4));
+      t = fe_add(t, fe_mul(fe_mul(r, ql), q.logic_sep));
+    }
+  }
   // permutation: alpha [ z (a + bX + g)(b + bK1X + g)(c + bK2X + g)(d + bK3X + g)
   //                    - z_next (a + b s1 + g)(b + b s2 + g)(c + b s3 + g)(d + b s4 + g) ]
   //              + (z - 1) L1(X) alpha^2

@@ -140,6 +140,9 @@ class Constraint:
     def range(self, v):
         return self._set("q_range", v)
 
+    def logic(self, v):
+        return self._set("q_logic", v)
+
     def public(self, v):
         self.c.has_public = 1
         self.c.public_input = _fr(v)
@@ -227,6 +230,75 @@ class Plonk:
 
     def component_boolean(self, a: int):
         _check(_bind().plk_composer_component_boolean(self._h, a), "component_boolean")
+
+    # ---- arithmetic-gate gadgets, restating src/lib.rs on top of the gate calls ----------
+    def component_decomposition(self, scalar: int, n: int):
+        """lib.rs:877-909: bits of `scalar` (LSB first, N of them), each boolean-constrained,
+        recombined with gate_add and asserted equal to the scalar (2N + 1 gates)."""
+        assert 0 < n <= 256
+        value = self[scalar]
+        acc = self.ZERO
+        bits = []
+        for i in range(n):
+            d = self.append_witness((value >> i) & 1)
+            self.component_boolean(d)
+            acc = self.gate_add(Constraint().left(pow(2, i, R_MOD)).right(1).a(d).b(acc))
+            bits.append(d)
+        self.assert_equal(acc, scalar)
+        return bits
+
+    def component_select(self, bit: int, a: int, b: int) -> int:
+        """lib.rs:959-990: bit ? a : b."""
+        bit_times_a = self.gate_mul(Constraint().mult(1).a(bit).b(a))
+        one_min_bit = self.gate_add(Constraint().left(-1).constant(1).a(bit))
+        one_min_bit_b = self.gate_mul(Constraint().mult(1).a(one_min_bit).b(b))
+        return self.gate_add(Constraint().left(1).right(1).a(one_min_bit_b).b(bit_times_a))
+
+    def component_select_one(self, bit: int, value: int) -> int:
+        """lib.rs:996-1020: bit ? value : 1."""
+        b, v = self[bit], self[value]
+        f_x = self.append_witness((1 - b + b * v) % R_MOD)
+        self.append_gate(Constraint().mult(1).left(-1).output(-1).constant(1)
+                         .a(bit).b(value).o(f_x))
+        return f_x
+
+    def component_select_zero(self, bit: int, value: int) -> int:
+        """lib.rs:1047-1057: bit ? value : 0."""
+        return self.gate_mul(Constraint().mult(1).a(bit).b(value))
+
+    def append_logic_and(self, a: int, b: int, num_bits: int) -> int:
+        """lib.rs:738-745"""
+        return self._append_logic_component(a, b, num_bits, False)
+
+    def append_logic_xor(self, a: int, b: int, num_bits: int) -> int:
+        """lib.rs:754-761"""
+        return self._append_logic_component(a, b, num_bits, True)
+
+    def _append_logic_component(self, a: int, b: int, num_bits: int, xor: bool) -> int:
+        """lib.rs:284-391: 2-bit quads of the low num_bits of a and b, most significant
+        first, accumulated 4x per gate (a, b, d wires: left, right, output accumulators; c:
+        the quad product), q_logic = q_c = 1 (AND) or -1 (XOR), closed by a zero gate."""
+        num_bits = min(num_bits, 256)
+        num_quads = num_bits >> 1
+        av, bv = self[a], self[b]
+        a_bits = [(av >> (num_bits - 1 - j)) & 1 for j in range(num_bits)]
+        b_bits = [(bv >> (num_bits - 1 - j)) & 1 for j in range(num_bits)]
+        sel = -1 if xor else 1
+        con = Constraint().logic(sel).constant(sel)
+        left = right = out = 0
+        for i in range(num_quads):
+            lq = (a_bits[2 * i] << 1) + a_bits[2 * i + 1]
+            rq = (b_bits[2 * i] << 1) + b_bits[2 * i + 1]
+            oq = (lq ^ rq) if xor else (lq & rq)
+            left, right, out = left * 4 + lq, right * 4 + rq, out * 4 + oq
+            wa, wb = self.append_witness(left), self.append_witness(right)
+            wc, wd = self.append_witness(lq * rq), self.append_witness(out)
+            con.o(wc)
+            self.append_custom_gate(con)
+            con.a(wa).b(wb).d(wd)
+        d = con.c.d
+        self.append_custom_gate(Constraint().a(con.c.a).b(con.c.b).d(d))
+        return d
 
     def component_range(self, a: int, num_bits: int):
         _check(_bind().plk_composer_component_range(self._h, a, num_bits), "component_range")

@@ -27,7 +27,7 @@
  * Randomness: the blinding scalars come from SplitMix64(seed), 4 words per scalar, top word
  * masked to 255 bits, rejection-sampled below r — the GPU prover consumes the
  * same stream in the same order (a, b, c, d: 2 each; z: 3).
- * Widgets restated: arithmetic and range; logic / fixed-base / variable-base selectors are
+ * Widgets restated: arithmetic, range and logic; fixed-base / variable-base selectors are
  * rejected (ORC_E_UNSUPPORTED), as the GPU build does.
  */
 #include "plk_oracle.c"
@@ -287,6 +287,89 @@ void orc_merlin_test(uint8_t* out32) {
   tr_challenge_bytes(&t, "challenge", out32, 32);
 }
 
+/* -------------------------------------------------------------------- logic widget */
+static void fr_small(uint64_t* r, uint64_t v) { fr_from_u64(r, v); }
+static void fr_delta(uint64_t* r, const uint64_t* f) { /* f (f - 1)(f - 2)(f - 3) */
+  fr_t k, t, u;
+  fr_set(u, f);
+  fr_small(k, 1);
+  FR_SUB(t, f, k);
+  FR_MUL(u, u, t);
+  fr_small(k, 2);
+  FR_SUB(t, f, k);
+  FR_MUL(u, u, t);
+  fr_small(k, 3);
+  FR_SUB(t, f, k);
+  FR_MUL(r, u, t);
+}
+/* dusk-plonk logic gate (zksnarks LogicGate widget, un-vendored): with quads
+ * a' = a_next - 4a, b' = b_next - 4b, d' = d_next - 4d and w = c:
+ *   D(a') + D(b') k + D(d') k^2 + (w - a'b') k^3 + xor_and(a', b', w, d', q_c) k^4
+ * xor_and = 3(a' + b' + d') - 2F + q_c (9d' - 3(a' + b')),
+ * F = w (w (4w - 18(a' + b') + 81) + 18(a'^2 + b'^2) - 81(a' + b') + 83) */
+static void logic_terms(uint64_t* out, const uint64_t* a, const uint64_t* an, const uint64_t* b,
+                        const uint64_t* bn, const uint64_t* w, const uint64_t* d,
+                        const uint64_t* dn, const uint64_t* qc, fr_t* lk) {
+  fr_t four, qa, qb, qd, t, u, sum, k;
+  fr_small(four, 4);
+  FR_MUL(t, four, a);
+  FR_SUB(qa, an, t);
+  FR_MUL(t, four, b);
+  FR_SUB(qb, bn, t);
+  FR_MUL(t, four, d);
+  FR_SUB(qd, dn, t);
+  fr_delta(sum, qa);
+  fr_delta(t, qb);
+  FR_MUL(t, t, lk[1]);
+  FR_ADD(sum, sum, t);
+  fr_delta(t, qd);
+  FR_MUL(t, t, lk[2]);
+  FR_ADD(sum, sum, t);
+  FR_MUL(t, qa, qb);
+  FR_SUB(t, w, t);
+  FR_MUL(t, t, lk[3]);
+  FR_ADD(sum, sum, t);
+  /* F */
+  fr_t ab, f;
+  FR_ADD(ab, qa, qb);
+  fr_small(k, 4);
+  FR_MUL(f, k, w);
+  fr_small(k, 18);
+  FR_MUL(t, k, ab);
+  FR_SUB(f, f, t);
+  fr_small(k, 81);
+  FR_ADD(f, f, k);
+  FR_MUL(f, f, w);
+  FR_MUL(t, qa, qa);
+  FR_MUL(u, qb, qb);
+  FR_ADD(t, t, u);
+  fr_small(k, 18);
+  FR_MUL(t, t, k);
+  FR_ADD(f, f, t);
+  fr_small(k, 81);
+  FR_MUL(t, k, ab);
+  FR_SUB(f, f, t);
+  fr_small(k, 83);
+  FR_ADD(f, f, k);
+  FR_MUL(f, f, w);
+  /* e = 3(a' + b' + d') - 2F ; bb = q_c (9d' - 3(a' + b')) */
+  fr_t e, bb;
+  FR_ADD(t, ab, qd);
+  fr_small(k, 3);
+  FR_MUL(e, k, t);
+  FR_ADD(t, f, f);
+  FR_SUB(e, e, t);
+  fr_small(k, 9);
+  FR_MUL(bb, k, qd);
+  fr_small(k, 3);
+  FR_MUL(t, k, ab);
+  FR_SUB(bb, bb, t);
+  FR_MUL(bb, bb, qc);
+  FR_ADD(t, bb, e);
+  FR_MUL(t, t, lk[4]);
+  FR_ADD(out, sum, t);
+}
+
 /* ------------------------------------------------------------------------- circuit */
 /* selector order of plk_constraint / the composer */
 enum { S_QM, S_QL, S_QR, S_QO, S_Q4, S_QC, S_QARITH, S_QRANGE, S_QLOGIC, S_QFIXED, S_QVAR, S_COUNT };
@@ -347,9 +430,7 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   const size_t GW = 51; /* u64 words per plk_constraint: 11 selectors, 6 u32, public input */
   for (size_t i = 0; i < m; ++i) {
     const uint64_t* g = gates + GW * i;
-    if (!fr_is_zero(g + 4 * S_QLOGIC) || !fr_is_zero(g + 4 * S_QFIXED) ||
-        !fr_is_zero(g + 4 * S_QVAR))
-      return ORC_E_UNSUPPORTED;
+    if (!fr_is_zero(g + 4 * S_QFIXED) || !fr_is_zero(g + 4 * S_QVAR)) return ORC_E_UNSUPPORTED;
     const uint32_t* w = (const uint32_t*)(g + 44);
     for (int c = 0; c < 4; ++c)
       if (w[c] >= nw) return ORC_E_ARG;
@@ -427,10 +508,11 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   }
   if (vk_out) memcpy(vk_out, vk, sizeof vk);
   /* 8n coset evaluations of selectors and sigmas (key.rs:220-245) */
-  static const int sel8_src[8] = {S_QM, S_QL, S_QR, S_QO, S_Q4, S_QC, S_QARITH, S_QRANGE};
-  uint64_t* sel8 = fr_alloc(8 * n8);
+  static const int sel8_src[9] = {S_QM, S_QL, S_QR, S_QO, S_Q4, S_QC, S_QARITH, S_QRANGE,
+                                  S_QLOGIC};
+  uint64_t* sel8 = fr_alloc(9 * n8);
   uint64_t* sig8 = fr_alloc(4 * n8);
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < 9; ++j) {
     memcpy(sel8 + 4 * j * n8, qc + 4 * sel8_src[j] * n, 32 * n);
     ntt_timed(sel8 + 4 * j * n8, k + 3, 1, 1, threads, &tm[2]);
   }
@@ -441,8 +523,11 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   /* v_h over the 8n coset: (g w8^i)^n - 1 (key.rs:291) */
   uint64_t* vh = fr_alloc(n8);
   orc_vanishing(k + 3, n, vh);
-  int has_range = 0;
-  for (size_t i = 0; i < m && !has_range; ++i) has_range = !fr_is_zero(gates + GW * i + 4 * S_QRANGE);
+  int has_range = 0, has_logic = 0;
+  for (size_t i = 0; i < m; ++i) {
+    has_range |= !fr_is_zero(gates + GW * i + 4 * S_QRANGE);
+    has_logic |= !fr_is_zero(gates + GW * i + 4 * S_QLOGIC);
+  }
   tm[0] = now_ns() - t_start;
 
   /* ==================================================================== create_proof */
@@ -563,10 +648,10 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   }
   t0 = now_ns();
   tr_append_commitment(&tr, "z", zcom);
-  fr_t alpha, range_sep, tmpc;
+  fr_t alpha, range_sep, logic_sep, tmpc;
   tr_challenge_scalar(&tr, "alpha", alpha);
   tr_challenge_scalar(&tr, "range separation challenge", range_sep);
-  tr_challenge_scalar(&tr, "logic separation challenge", tmpc);
+  tr_challenge_scalar(&tr, "logic separation challenge", logic_sep);
   tr_challenge_scalar(&tr, "fixed base separation challenge", tmpc);
   tr_challenge_scalar(&tr, "variable base separation challenge", tmpc);
   t_tr += now_ns() - t0;
@@ -590,10 +675,13 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   fr_set(l18, alpha2);
   ntt_timed(l18, k, -1, 0, threads, &tm[2]);
   ntt_timed(l18, k + 3, 1, 1, threads, &tm[2]);
-  fr_t kappa, kappa2, kappa3;
+  fr_t kappa, kappa2, kappa3, lk[5];
   FR_MUL(kappa, range_sep, range_sep);
   FR_MUL(kappa2, kappa, kappa);
   FR_MUL(kappa3, kappa2, kappa);
+  fr_set(lk[0], FR_ONE); /* logic: 1, k, k^2, k^3, k^4 with k = logic_sep^2 */
+  FR_MUL(lk[1], logic_sep, logic_sep);
+  for (int j = 2; j < 5; ++j) FR_MUL(lk[j], lk[j - 1], lk[1]);
   uint64_t* quot = fr_alloc(n8);
   {
     const uint64_t tq = now_ns();
@@ -642,6 +730,17 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
         }
         FR_MUL(sum, sum, sel8 + 4 * (7 * n8 + i));
         FR_MUL(sum, sum, range_sep);
+        FR_ADD(acc, acc, sum);
+      }
+      /* logic: sep q_logic (D(a') + D(b') k + D(d') k^2 + (c - a'b') k^3 + xor_and k^4) */
+      if (has_logic) {
+        const uint64_t* an = ev[1] + 4 * (i + 8);
+        const uint64_t* bn = ev[2] + 4 * (i + 8);
+        const uint64_t* dn = ev[4] + 4 * (i + 8);
+        fr_t sum;
+        logic_terms(sum, a, an, b, bn, c, d, dn, sel8 + 4 * (5 * n8 + i), lk);
+        FR_MUL(sum, sum, sel8 + 4 * (8 * n8 + i));
+        FR_MUL(sum, sum, logic_sep);
         FR_ADD(acc, acc, sum);
       }
       fr_set(t1 + 4 * i, acc);
@@ -764,6 +863,12 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
       }
       FR_MUL(sum, sum, range_sep);
       poly_axpy(rc, qc + 4 * S_QRANGE * n, n, sum);
+    }
+    if (has_logic) {
+      fr_t sum;
+      logic_terms(sum, a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, qc_e, lk);
+      FR_MUL(sum, sum, logic_sep);
+      poly_axpy(rc, qc + 4 * S_QLOGIC * n, n, sum);
     }
     /* identity: z(X) (a + b z + g)(b + b K1 z + g)(c + b K2 z + g)(d + b K3 z + g) alpha */
     fr_t bz, idc;

@@ -87,7 +87,63 @@ def ranged(a, bits):
 
 R_MOD = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 
+
+def decomposition(a, n, flip=None):
+    """tests/decomposition.rs DummyCircuit<N>: witness bits asserted equal to
+    component_decomposition(a); `flip` corrupts one bit (the negative case)."""
+    def f(cs):
+        w_a = cs.append_witness(a)
+        bits = [(a >> i) & 1 for i in range(n)]
+        if flip is not None:
+            bits[flip] ^= 1
+        w_bits = [cs.append_witness(b) for b in bits]
+        for w, b in zip(w_bits, cs.component_decomposition(w_a, n)):
+            cs.assert_equal(w, b)
+    return f
+
+
+def selects(bit, a, b):
+    """component_select / _one / _zero outputs pinned with assert_equal_constant."""
+    def f(cs):
+        wb, wa, wv = cs.append_witness(bit), cs.append_witness(a), cs.append_witness(b)
+        cs.component_boolean(wb)
+        s = cs.component_select(wb, wa, wv)
+        cs.assert_equal_constant(s, a if bit else b)
+        s1 = cs.component_select_one(wb, wa)
+        cs.assert_equal_constant(s1, a if bit else 1)
+        s0 = cs.component_select_zero(wb, wa)
+        cs.assert_equal_constant(s0, a if bit else 0)
+    return f
+
+def logic(a, b, bits, xor, wrong=False):
+    """tests/logic.rs DummyCircuit: append_logic_and / _xor of the low `bits` bits, asserted
+    equal to the expected value (`wrong` asserts a different value: the negative case)."""
+    def f(cs):
+        mask = (1 << bits) - 1
+        aa, bb = a & mask, b & mask
+        c = (aa ^ bb) if xor else (aa & bb)
+        c >>= bits & 1  # odd counts: 2-bit quads cover the top bits - 1 bits (lib.rs:291)
+        if wrong:
+            c ^= 1
+        wa, wb, wc = cs.append_witness(aa), cs.append_witness(bb), cs.append_witness(c)
+        wx = cs.append_logic_xor(wa, wb, bits) if xor else cs.append_logic_and(wa, wb, bits)
+        cs.assert_equal(wc, wx)
+    return f
+
+
+A_RND = 0x3A5F0E29B8C1D47265E0F1A2B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6
+B_RND = 0x2F1E3D4C5B6A79881726354453627180A9B8C7D6E5F40312233445566778899A
+
 CASES = [
+    ("and_254", logic(A_RND, B_RND, 254, False), 51),
+    ("and_30", logic(A_RND, B_RND, 30, False), 52),
+    ("and_0", logic(A_RND, B_RND, 0, False), 53),
+    ("and_55", logic(A_RND, B_RND, 55, False), 54),
+    ("xor_254", logic(A_RND, B_RND, 254, True), 55),
+    ("xor_30", logic(A_RND, B_RND, 30, True), 56),
+    ("decomposition_256", decomposition(0x1234567890ABCDEF1122334455667788 * 7919, 256), 41),
+    ("select_1", selects(1, 77, 99), 42),
+    ("select_0", selects(0, 77, 99), 43),
     ("range_u64max_76", ranged(2**64 - 1, 76), 31),
     ("range_7_76", ranged(7, 76), 32),
     ("range_odd_77", ranged(1, 77), 33),
@@ -132,7 +188,12 @@ def test_oracle_proof_verifies(plk, oracle, name, fn, seed):
 
 
 @pytest.mark.parametrize("fn", [boolean(2), ranged((R_MOD - 2**77) % R_MOD, 76),
-                                ranged(2**76, 76)], ids=["boolean2", "range_neg", "range_2^76"])
+                                ranged(2**76, 76),
+                                decomposition(0x1234567890ABCDEF * 31337, 256, flip=10),
+                                logic(A_RND, B_RND, 254, False, wrong=True),
+                                logic(A_RND, B_RND, 64, True, wrong=True)],
+                         ids=["boolean2", "range_neg", "range_2^76", "decomposition_flip",
+                              "and_wrong", "xor_wrong"])
 def test_oracle_rejects_unsatisfied(plk, oracle, fn):
     tau_limbs, _ = tau_for(1)
     cs = build(fn)

@@ -104,7 +104,7 @@ def verify(vd, proof, public_inputs, tau: int) -> None:
     append_commitment(t, b"z", C["z_comm"])
     alpha = challenge_scalar(t, b"alpha")
     range_sep = challenge_scalar(t, b"range separation challenge")
-    challenge_scalar(t, b"logic separation challenge")
+    logic_sep = challenge_scalar(t, b"logic separation challenge")
     challenge_scalar(t, b"fixed base separation challenge")
     challenge_scalar(t, b"variable base separation challenge")
     for lab, c in ((b"t_low", "t_low_comm"), (b"t_mid", "t_mid_comm"), (b"t_high", "t_high_comm"),
@@ -160,7 +160,21 @@ def verify(vd, proof, public_inputs, tau: int) -> None:
               + delta(e.a_eval - 4 * e.b_eval) * kap * kap
               + delta(e.d_next_eval - 4 * e.a_eval) * kap * kap * kap) % r
         terms.append((vk["q_range"], rr * range_sep))
-    for lab in ("q_logic", "q_fixed_group_add", "q_variable_group_add"):
+    if vk["q_logic"] is not None:  # logic::linearize (dusk-plonk LogicGate; zksnarks)
+        def delta(f):
+            return f * (f - 1) * (f - 2) * (f - 3) % r
+        k = logic_sep * logic_sep % r
+        qa = (e.a_next_eval - 4 * e.a_eval) % r
+        qb = (e.b_next_eval - 4 * e.b_eval) % r
+        qd = (e.d_next_eval - 4 * e.d_eval) % r
+        w = e.c_eval
+        f = w * (w * (4 * w - 18 * (qa + qb) + 81) + 18 * (qa * qa + qb * qb)
+                 - 81 * (qa + qb) + 83) % r
+        xor_and = (3 * (qa + qb + qd) - 2 * f + e.q_c_eval * (9 * qd - 3 * (qa + qb))) % r
+        lt = (delta(qa) + delta(qb) * k + delta(qd) * k ** 2 + (w - qa * qb) * k ** 3
+              + xor_and * k ** 4) % r
+        terms.append((vk["q_logic"], lt * logic_sep))
+    for lab in ("q_fixed_group_add", "q_variable_group_add"):
         if vk[lab] is not None:
             raise VerificationError(f"{lab} widget not restated")
     bz = beta * z % r
