@@ -55,7 +55,7 @@ const char* plk_status_str(int s) {
     case PLK_E_DEVICE: return "HIP device error";
     case PLK_E_OOM: return "device out of memory";
     case PLK_E_NODEV: return "no GPU available";
-    case PLK_E_UNSUPPORTED: return "circuit uses an unsupported widget (logic / curve)";
+    case PLK_E_UNSUPPORTED: return "unsupported feature";
     default: return "unknown status";
   }
 }

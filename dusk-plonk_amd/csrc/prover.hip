@@ -300,6 +300,16 @@ int key_commit(plk_key* key, const std::vector<const Fr*>& ptrs, const std::vect
   return overall;
 }
 
+// JubJub twisted-Edwards d = -10240/10241 mod r
+// (0x2a9318e74bfa2b48f5fd9207e6bd7fd4292d7f6d37579d2601065fd6d6343eb1), Montgomery form
+Fr edwards_d() {
+  static const uint32_t w[8] = {0xd6343eb1u, 0x01065fd6u, 0x37579d26u, 0x292d7f6du,
+                                0xe6bd7fd4u, 0xf5fd9207u, 0x4bfa2b48u, 0x2a9318e7u};
+  Fr x;
+  for (int i = 0; i < 8; ++i) x.v[i] = w[i];
+  return fe_to_mont(x);
+}
+
 Fr d2h_fr(const Fr* p, hipStream_t s) {
   thread_local PinnedBuf pin;
   if (pin.alloc(sizeof(Fr)) != PLK_OK) return fe_zero<FrCfg>();
@@ -625,10 +635,10 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     if (k + 3 > 27) return PLK_E_ARG;
     for (uint64_t i = 0; i < m; ++i) {
       const Gate g = gate_unpack(cs, i);
-      if (!fe_is_zero(g.q[QFIXED]) || !fe_is_zero(g.q[QVAR]))
-        return PLK_E_UNSUPPORTED;  // curve widgets: next round
       if (!fe_is_zero(g.q[QRANGE])) key->has_range = true;
       if (!fe_is_zero(g.q[QLOGIC])) key->has_logic = true;
+      if (!fe_is_zero(g.q[QFIXED])) key->has_fixed = true;
+      if (!fe_is_zero(g.q[QVAR])) key->has_var = true;
     }
     TRY(plk_domain_get(ctx, k, &key->dom));
     TRY(plk_domain_get(ctx, k + 3, &key->dom8));
@@ -692,9 +702,12 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
 
     // 4. 8n coset evaluations (key.rs:220-245) and v_h over the coset (key.rs:291)
     TRY(key->sel8.alloc(SEL_COUNT8 * n8 * sizeof(Fr)));
-    const int sel_src[SEL_COUNT8] = {QM, QL, QR, QO, Q4, QC, QARITH, QRANGE, QLOGIC};
-    for (int j = 0; j < SEL_COUNT8; ++j)
-      TRY(ntt_run(key->dom8, qc + sel_src[j] * n, key->sel8.as<Fr>() + j * n8, n, 1, 1, nullptr, s, 1));
+    const int sel_src[SEL_COUNT8] = {QM, QL, QR, QO, Q4, QC, QARITH, QRANGE, QLOGIC, QFIXED, QVAR};
+    const bool sel_used[SEL_COUNT8] = {true, true, true, true, true, true, true, key->has_range,
+                                       key->has_logic, key->has_fixed, key->has_var};
+    for (int j = 0; j < SEL_COUNT8; ++j)  // unused widget selectors are never read
+      if (sel_used[j])
+        TRY(ntt_run(key->dom8, qc + sel_src[j] * n, key->sel8.as<Fr>() + j * n8, n, 1, 1, nullptr, s, 1));
     TRY(key->sigma8.alloc(4 * n8 * sizeof(Fr)));
     for (int c = 0; c < 4; ++c)
       TRY(ntt_run(key->dom8, sc + c * n, key->sigma8.as<Fr>() + c * n8, n, 1, 1, nullptr, s, 1));
@@ -856,8 +869,8 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     const Fr alpha = tr.challenge_scalar("alpha");
     const Fr range_sep = tr.challenge_scalar("range separation challenge");
     const Fr logic_sep = tr.challenge_scalar("logic separation challenge");
-    (void)tr.challenge_scalar("fixed base separation challenge");
-    (void)tr.challenge_scalar("variable base separation challenge");
+    const Fr fixed_sep = tr.challenge_scalar("fixed base separation challenge");
+    const Fr var_sep = tr.challenge_scalar("variable base separation challenge");
     Fr* pil = key->pi_lag.as<Fr>();
     PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
     // pin_small: [0, #pi) PI values uploaded here, [#pi, #pi + 16) the evaluations read
@@ -908,6 +921,16 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     qa.lk3 = fe_mul(qa.lk2, qa.lk);
     qa.lk4 = fe_mul(qa.lk3, qa.lk);
     qa.has_logic = key->has_logic ? 1 : 0;
+    qa.fixed_sep = fixed_sep;
+    qa.fk = fe_sqr(fixed_sep);
+    qa.fk2 = fe_sqr(qa.fk);
+    qa.fk3 = fe_mul(qa.fk2, qa.fk);
+    qa.var_sep = var_sep;
+    qa.vk = fe_sqr(var_sep);
+    qa.vk2 = fe_sqr(qa.vk);
+    qa.edwards_d = edwards_d();
+    qa.has_fixed = key->has_fixed ? 1 : 0;
+    qa.has_var = key->has_var ? 1 : 0;
     for (int j = 0; j < 8; ++j) qa.vh_inv[j] = key->vh_inv[j];
     TRY(pk_quotient(qa, s));
     Fr* tc = key->t_coef.as<Fr>();
@@ -986,6 +1009,16 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       r = fe_add(r, fe_mul(fe_sub(c_e, fe_mul(qa_, qb_)), qa.lk3));
       r = fe_add(r, fe_mul(logic_xor_and(qa_, qb_, c_e, qd_, qc_e), qa.lk4));
       term(qc + QLOGIC * n, n, fe_mul(r, logic_sep));
+    }
+    if (key->has_fixed) {  // curve_scalar::linearize at the evaluations (q_l/q_r/q_c evals)
+      const Fr w = widget_fixed_base(a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, ql_e, qr_e, qc_e,
+                                     qa.fk, qa.fk2, qa.fk3, qa.edwards_d);
+      term(qc + QFIXED * n, n, fe_mul(w, fixed_sep));
+    }
+    if (key->has_var) {  // curve_addtion::linearize
+      const Fr w = widget_var_base(a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, qa.vk, qa.vk2,
+                                   qa.edwards_d);
+      term(qc + QVAR * n, n, fe_mul(w, var_sep));
     }
     // z(X) * [(a + b z + g)(b + b K1 z + g)(c + b K2 z + g)(d + b K3 z + g) alpha + L1(z) alpha^2]
     const Fr bz = fe_mul(beta, zeta);

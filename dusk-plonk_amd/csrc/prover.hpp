@@ -18,7 +18,7 @@ struct BlindArgs {
 
 // selector rows of the 8n evaluation table
 enum { SEL_QM = 0, SEL_QL, SEL_QR, SEL_QO, SEL_Q4, SEL_QC, SEL_QARITH, SEL_QRANGE, SEL_QLOGIC,
-       SEL_COUNT8 };
+       SEL_QFIXED, SEL_QVAR, SEL_COUNT8 };
 
 struct QuotientArgs {
   const Fr *a, *b, *c, *d, *z, *pi, *l1a, *sel, *sigma, *elements8;
@@ -27,7 +27,10 @@ struct QuotientArgs {
   Fr g, alpha, beta, gamma, k1, k2, k3;
   Fr range_sep, kappa, kappa2, kappa3;
   Fr logic_sep, lk, lk2, lk3, lk4;  // logic separation challenge and its kappa powers
-  int has_range, has_logic;
+  Fr fixed_sep, fk, fk2, fk3;        // fixed-base scalar mul: sep, kappa = sep^2, ^2, ^3
+  Fr var_sep, vk, vk2;               // variable-base addition: sep, kappa = sep^2, ^2
+  Fr edwards_d;                      // JubJub d = -10240/10241
+  int has_range, has_logic, has_fixed, has_var;
   Fr vh_inv[8];
 };
 
@@ -66,6 +69,47 @@ PLK_HD Fr logic_xor_and(const Fr& a, const Fr& b, const Fr& w, const Fr& c,
   const Fr e = fe_sub(fe_mul(k(3), fe_add(ab, c)), fe_dbl(f));
   const Fr bb = fe_mul(qc, fe_sub(fe_mul(k(9), c), fe_mul(k(3), ab)));
   return fe_add(bb, e);
+}
+
+// Fixed-base scalar multiplication widget (dusk-plonk ecc/scalar_mul/fixed_base; zksnarks
+// curve_scalar, un-vendored): accumulators (a, b) = point, d = scalar accumulator,
+// c = xy_alpha, q_l / q_r / q_c = x_beta / y_beta / x_beta y_beta of the gate's multiple.
+//   bit = d' - 2d;  bit (bit - 1)(bit + 1) + (bit q_c - c) k + x-check k^2 + y-check k^3
+PLK_HD Fr widget_fixed_base(const Fr& ax, const Fr& ax_n, const Fr& ay, const Fr& ay_n,
+                            const Fr& xy_alpha, const Fr& acc, const Fr& acc_n,
+                            const Fr& x_beta, const Fr& y_beta, const Fr& xy_beta, const Fr& k,
+                            const Fr& k2, const Fr& k3, const Fr& d) {
+  const Fr one = fe_one<FrCfg>();
+  const Fr bit = fe_sub(acc_n, fe_dbl(acc));
+  const Fr bit_consistency = fe_mul(fe_mul(bit, fe_sub(bit, one)), fe_add(bit, one));
+  const Fr y_alpha = fe_add(fe_mul(fe_sqr(bit), fe_sub(y_beta, one)), one);
+  const Fr x_alpha = fe_mul(x_beta, bit);
+  const Fr xy_consistency = fe_mul(fe_sub(fe_mul(bit, xy_beta), xy_alpha), k);
+  const Fr prod = fe_mul(fe_mul(fe_mul(xy_alpha, ax), ay), d);
+  const Fr x_lhs = fe_add(ax_n, fe_mul(ax_n, prod));
+  const Fr x_rhs = fe_add(fe_mul(ax, y_alpha), fe_mul(ay, x_alpha));
+  const Fr y_lhs = fe_sub(ay_n, fe_mul(ay_n, prod));
+  const Fr y_rhs = fe_add(fe_mul(ay, y_alpha), fe_mul(ax, x_alpha));
+  Fr id = fe_add(bit_consistency, xy_consistency);
+  id = fe_add(id, fe_mul(fe_sub(x_lhs, x_rhs), k2));
+  id = fe_add(id, fe_mul(fe_sub(y_lhs, y_rhs), k3));
+  return id;
+}
+
+// Variable-base addition widget (dusk-plonk ecc/curve_addition; zksnarks curve_addtion):
+// gate (x1, y1, x2, y2), next row (x3, y3, ., x1 y2):
+//   (x1 y2 - x1y2') + (x1y2' + y1 x2 - x3 (1 + d x1y2' y1 x2)) k
+//                   + (y1 y2 + x1 x2 - y3 (1 - d x1y2' y1 x2)) k^2
+PLK_HD Fr widget_var_base(const Fr& x1, const Fr& x3, const Fr& y1, const Fr& y3, const Fr& x2,
+                          const Fr& y2, const Fr& x1y2, const Fr& k, const Fr& k2, const Fr& d) {
+  const Fr xy_consistency = fe_sub(fe_mul(x1, y2), x1y2);
+  const Fr y1x2 = fe_mul(y1, x2);
+  const Fr y1y2 = fe_mul(y1, y2);
+  const Fr x1x2 = fe_mul(x1, x2);
+  const Fr dprod = fe_mul(fe_mul(d, x1y2), y1x2);
+  const Fr x3c = fe_sub(fe_add(x1y2, y1x2), fe_add(x3, fe_mul(x3, dprod)));
+  const Fr y3c = fe_sub(fe_add(y1y2, x1x2), fe_sub(y3, fe_mul(y3, dprod)));
+  return fe_add(fe_add(xy_consistency, fe_mul(x3c, k)), fe_mul(y3c, k2));
 }
 
 int pk_gather_wires(const Fr* witness, const uint32_t* idx, uint64_t m, uint64_t n, Fr* out,
@@ -132,7 +176,7 @@ struct plk_key {
   uint32_t k = 0;
   plk_domain* dom = nullptr;   // n
   plk_domain* dom8 = nullptr;  // 8n
-  bool has_range = false, has_logic = false;
+  bool has_range = false, has_logic = false, has_fixed = false, has_var = false;
   // device-resident proving key
   plk::DevBuf q_coef;       // 11 x n selector coefficient polys
   plk::DevBuf sel8;         // SEL_COUNT8 x 8n coset evaluations

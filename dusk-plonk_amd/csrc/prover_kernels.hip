@@ -238,6 +238,23 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
       t = fe_add(t, fe_mul(fe_mul(r, ql), q.logic_sep));
     }
   }
+  if (q.has_fixed) {
+    const Fr qf = ldf(&q.sel[SEL_QFIXED * N + i]);
+    if (!fe_is_zero(qf)) {
+      const Fr w = widget_fixed_base(a, ldf(&q.a[nx]), b, ldf(&q.b[nx]), c, d, ldf(&q.d[nx]),
+                                     ldf(&q.sel[SEL_QL * N + i]), ldf(&q.sel[SEL_QR * N + i]),
+                                     ldf(&q.sel[SEL_QC * N + i]), q.fk, q.fk2, q.fk3, q.edwards_d);
+      t = fe_add(t, fe_mul(fe_mul(w, qf), q.fixed_sep));
+    }
+  }
+  if (q.has_var) {
+    const Fr qv = ldf(&q.sel[SEL_QVAR * N + i]);
+    if (!fe_is_zero(qv)) {
+      const Fr w = widget_var_base(a, ldf(&q.a[nx]), b, ldf(&q.b[nx]), c, d, ldf(&q.d[nx]),
+                                   q.vk, q.vk2, q.edwards_d);
+      t = fe_add(t, fe_mul(fe_mul(w, qv), q.var_sep));
+    }
+  }
   // permutation: alpha [ z (a + bX + g)(b + bK1X + g)(c + bK2X + g)(d + bK3X + g)
   //                    - z_next (a + b s1 + g)(b + b s2 + g)(c + b s3 + g)(d + b s4 + g) ]
   //              + (z - 1) L1(X) alpha^2

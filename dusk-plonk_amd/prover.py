@@ -165,6 +165,57 @@ class Constraint:
         return self
 
 
+# ---- JubJub (twisted Edwards -x^2 + y^2 = 1 + d x^2 y^2 over Fr), the composer's curve C ----
+EDWARDS_D = (-10240 * pow(10241, -1, R_MOD)) % R_MOD
+JUBJUB_IDENTITY = (0, 1)
+# dusk-jubjub / jub_jub GENERATOR (on the curve, prime-order subgroup; tests/test_ecc)
+JUBJUB_GENERATOR = (0x3FD2814C43AC65A6F1FBF02D0FD6CCE62E3EBB21FD6C54ED4DF7B7FFEC7BEACA, 0x12)
+JUBJUB_ORDER = 0x0E7DB4EA6533AFA906673B0101343B00A6682093CCC81082D0970E5ED6F72CB7
+
+
+def jubjub_add(p, q):
+    (x1, y1), (x2, y2) = p, q
+    t = EDWARDS_D * x1 * x2 * y1 * y2 % R_MOD
+    x3 = (x1 * y2 + y1 * x2) * pow(1 + t, -1, R_MOD) % R_MOD
+    y3 = (y1 * y2 + x1 * x2) * pow(1 - t, -1, R_MOD) % R_MOD
+    return (x3, y3)
+
+
+def jubjub_neg(p):
+    return ((-p[0]) % R_MOD, p[1])
+
+
+def jubjub_mul(p, k: int):
+    acc = JUBJUB_IDENTITY
+    for b in bin(k)[2:] if k > 0 else "":
+        acc = jubjub_add(acc, acc)
+        if b == "1":
+            acc = jubjub_add(acc, p)
+    return acc
+
+
+def windowed_naf(k: int, width: int = 2):
+    """compute_windowed_naf(scalar, width) (zkstd, un-vendored): signed digits, least
+    significant first, 256 entries; width 2 gives the NAF with digits in {-1, 0, 1}."""
+    out = [0] * 256
+    i = 0
+    while k >= 1:
+        if k & 1:
+            d = k % (1 << width)
+            if d >= 1 << (width - 1):
+                d -= 1 << width
+            out[i] = d
+            k -= d
+        k >>= 1
+        i += 1
+    return out
+
+
+class WitnessPoint:
+    def __init__(self, x: int, y: int):
+        self.x, self.y = x, y
+
+
 class Plonk:
     """The composer, Plonk<JubjubAffine> (src/lib.rs:103-115); construction = initialize()."""
 
@@ -299,6 +350,114 @@ class Plonk:
         d = con.c.d
         self.append_custom_gate(Constraint().a(con.c.a).b(con.c.b).d(d))
         return d
+
+    # ---- curve gadgets (lib.rs), JubJub points as pairs of witnesses ------------------
+    IDENTITY = WitnessPoint(0, 1)
+
+    def append_constant(self, v) -> int:
+        w = self.append_witness(v)
+        self.assert_equal_constant(w, v)
+        return w
+
+    def append_point(self, p) -> WitnessPoint:
+        """lib.rs:657-664"""
+        return WitnessPoint(self.append_witness(p[0]), self.append_witness(p[1]))
+
+    def append_constant_point(self, p) -> WitnessPoint:
+        """lib.rs:668-678"""
+        return WitnessPoint(self.append_constant(p[0]), self.append_constant(p[1]))
+
+    def append_public_point(self, p) -> WitnessPoint:
+        """lib.rs:683-700"""
+        pt = self.append_point(p)
+        self.assert_equal_constant(pt.x, 0, -p[0])
+        self.assert_equal_constant(pt.y, 0, -p[1])
+        return pt
+
+    def assert_equal_point(self, a: WitnessPoint, b: WitnessPoint):
+        """lib.rs:781-784"""
+        self.assert_equal(a.x, b.x)
+        self.assert_equal(a.y, b.y)
+
+    def assert_equal_public_point(self, point: WitnessPoint, p):
+        """lib.rs:789-805"""
+        self.assert_equal_constant(point.x, 0, -p[0])
+        self.assert_equal_constant(point.y, 0, -p[1])
+
+    def component_add_point(self, a: WitnessPoint, b: WitnessPoint) -> WitnessPoint:
+        """lib.rs:810-852: two gates, (x1, y1, x2, y2) with q_variable_group_add = 1 and
+        (x3, y3, ., x1 y2)."""
+        x1, y1, x2, y2 = self[a.x], self[a.y], self[b.x], self[b.y]
+        x3, y3 = jubjub_add((x1, y1), (x2, y2))
+        w_x1y2 = self.append_witness(x1 * y2 % R_MOD)
+        w_x3, w_y3 = self.append_witness(x3), self.append_witness(y3)
+        con = Constraint().a(a.x).b(a.y).o(b.x).d(b.y)
+        con._set("q_variable_group_add", 1)
+        self.append_custom_gate(con)
+        self.append_custom_gate(Constraint().a(w_x3).b(w_y3).d(w_x1y2))
+        return WitnessPoint(w_x3, w_y3)
+
+    def component_select_identity(self, bit: int, a: WitnessPoint) -> WitnessPoint:
+        """lib.rs:920-929: bit ? a : identity"""
+        return WitnessPoint(self.component_select_zero(bit, a.x),
+                            self.component_select_one(bit, a.y))
+
+    def component_select_point(self, bit: int, a: WitnessPoint, b: WitnessPoint):
+        """lib.rs:1028-1040"""
+        return WitnessPoint(self.component_select(bit, a.x, b.x),
+                            self.component_select(bit, a.y, b.y))
+
+    def component_mul_point(self, jubjub: int, point: WitnessPoint) -> WitnessPoint:
+        """lib.rs:932-954: double-and-add over the 252-bit decomposition."""
+        bits = self.component_decomposition(jubjub, 252)
+        result = self.IDENTITY
+        for bit in reversed(bits):
+            result = self.component_add_point(result, result)
+            result = self.component_add_point(result, self.component_select_identity(bit, point))
+        return result
+
+    def component_mul_generator(self, jubjub: int, generator=JUBJUB_GENERATOR) -> WitnessPoint:
+        """lib.rs:395-548: fixed-base multiplication by a width-2 wNAF over the 256
+        precomputed multiples 2^i G (constants in q_l, q_r, q_c), one gate per digit with
+        q_fixed_group_add = 1, point / scalar accumulators chained to the next gate."""
+        bits = 256
+        multiples = [generator]
+        for _ in range(1, bits):
+            multiples.append(jubjub_add(multiples[-1], multiples[-1]))
+        multiples.reverse()
+        scalar = self[jubjub]
+        wnaf = windowed_naf(scalar, 2)
+        scalar_acc, point_acc, xy_alphas = [0], [JUBJUB_IDENTITY], []
+        for i, entry in enumerate(reversed(wnaf)):
+            if entry == 0:
+                s_add, p_add = 0, JUBJUB_IDENTITY
+            elif entry == -1:
+                s_add, p_add = R_MOD - 1, jubjub_neg(multiples[i])
+            else:
+                s_add, p_add = 1, multiples[i]
+            scalar_acc.append((2 * scalar_acc[i] + s_add) % R_MOD)
+            point_acc.append(jubjub_add(point_acc[i], p_add))
+            xy_alphas.append(p_add[0] * p_add[1] % R_MOD)
+        for i in range(bits):
+            acc_x = self.append_witness(point_acc[i][0])
+            acc_y = self.append_witness(point_acc[i][1])
+            acc_bit = self.append_witness(scalar_acc[i])
+            if i == 0:
+                self.assert_equal_constant(acc_x, 0)
+                self.assert_equal_constant(acc_y, 1)
+                self.assert_equal_constant(acc_bit, 0)
+            x_beta, y_beta = multiples[i]
+            xy_alpha = self.append_witness(xy_alphas[i])
+            con = (Constraint().left(x_beta).right(y_beta).constant(x_beta * y_beta % R_MOD)
+                   .a(acc_x).b(acc_y).o(xy_alpha).d(acc_bit))
+            con._set("q_fixed_group_add", 1)
+            self.append_custom_gate(con)
+        acc_x = self.append_witness(point_acc[bits][0])
+        acc_y = self.append_witness(point_acc[bits][1])
+        last = self.append_witness(scalar_acc[bits])
+        self.append_gate(Constraint().a(acc_x).b(acc_y).d(last))
+        self.assert_equal(last, jubjub)
+        return WitnessPoint(acc_x, acc_y)
 
     def component_range(self, a: int, num_bits: int):
         _check(_bind().plk_composer_component_range(self._h, a, num_bits), "component_range")

@@ -43,7 +43,7 @@ typedef enum {
   PLK_E_DEVICE = 3,   /* HIP runtime error */
   PLK_E_OOM = 4,      /* device allocation failed */
   PLK_E_NODEV = 5,    /* no GPU visible / HIP unavailable */
-  PLK_E_UNSUPPORTED = 6 /* circuit uses a widget this backend does not prove yet */
+  PLK_E_UNSUPPORTED = 6 /* reserved: a feature this backend does not implement */
 } plk_status;
 
 typedef struct plk_ctx plk_ctx;
@@ -202,7 +202,8 @@ int plk_composer_export(const plk_composer* c, plk_constraint* gates, size_t cap
 
 /* PlonkKey::compile_with_circuit (src/key.rs:63-327): device-resident proving key for the
  * circuit's structure, committed against `srs` (trimmed to next_pow2(m + 6) + 8 points).
- * PLK_E_UNSUPPORTED for logic / curve-widget selectors (next round). */
+ * All five widgets are proven: arithmetic, range, logic, fixed-base scalar multiplication
+ * and variable-base addition (quotient_poly.rs:128-262, linearization_poly.rs:136-225). */
 int plk_key_compile(plk_srs* srs, const plk_composer* circuit, const char* label, plk_key** out);
 int plk_key_destroy(plk_key* key);
 /* n (padded domain), m (gates) and the 15 verifier-key commitments in transcript order

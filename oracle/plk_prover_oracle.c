@@ -27,8 +27,8 @@
  * Randomness: the blinding scalars come from SplitMix64(seed), 4 words per scalar, top word
  * masked to 255 bits, rejection-sampled below r — the GPU prover consumes the
  * same stream in the same order (a, b, c, d: 2 each; z: 3).
- * Widgets restated: arithmetic, range and logic; fixed-base / variable-base selectors are
- * rejected (ORC_E_UNSUPPORTED), as the GPU build does.
+ * Widgets restated: arithmetic, range, logic, fixed-base scalar multiplication and
+ * variable-base addition (the latter three from upstream dusk-plonk: parity unpinned).
  */
 #include "plk_oracle.c"
 
@@ -370,6 +370,92 @@ static void logic_terms(uint64_t* out, const uint64_t* a, const uint64_t* an, co
   FR_ADD(out, sum, t);
 }
 
+/* -------------------------------------------------------------------- curve widgets */
+/* JubJub twisted-Edwards d = -10240/10241 mod r, Montgomery */
+static void edwards_d(uint64_t* out) {
+  fr_t a, b;
+  fr_small(a, 10240);
+  fr_small(b, 10241);
+  fr_inv(b, b);
+  FR_MUL(a, a, b);
+  fr_neg(out, a);
+}
+/* fixed-base scalar mul (dusk-plonk ecc/scalar_mul/fixed_base; zksnarks curve_scalar):
+ * bit = d' - 2d; x_alpha = x_beta bit; y_alpha = bit^2 (y_beta - 1) + 1;
+ * bit (bit-1)(bit+1) + (bit xy_beta - c) k + (x' (1 + c a b d_E) - (a y_alpha + b x_alpha)) k^2
+ *   + (y' (1 - c a b d_E) - (b y_alpha + a x_alpha)) k^3    (a, b: point accumulator) */
+static void fixed_base_terms(uint64_t* out, const uint64_t* ax, const uint64_t* axn,
+                             const uint64_t* ay, const uint64_t* ayn, const uint64_t* xya,
+                             const uint64_t* acc, const uint64_t* accn, const uint64_t* xb,
+                             const uint64_t* yb, const uint64_t* xyb, fr_t* k,
+                             const uint64_t* ed) {
+  fr_t bit, t, u, bc, ya, xa, xy, prod, lhs, rhs, id, one;
+  fr_set(one, FR_ONE);
+  FR_ADD(t, acc, acc);
+  FR_SUB(bit, accn, t);
+  FR_SUB(t, bit, one);
+  FR_MUL(bc, bit, t);
+  FR_ADD(t, bit, one);
+  FR_MUL(bc, bc, t);
+  FR_MUL(t, bit, bit);
+  FR_SUB(u, yb, one);
+  FR_MUL(ya, t, u);
+  FR_ADD(ya, ya, one);
+  FR_MUL(xa, xb, bit);
+  FR_MUL(xy, bit, xyb);
+  FR_SUB(xy, xy, xya);
+  FR_MUL(xy, xy, k[1]);
+  FR_MUL(prod, xya, ax);
+  FR_MUL(prod, prod, ay);
+  FR_MUL(prod, prod, ed);
+  fr_set(id, bc);
+  FR_ADD(id, id, xy);
+  FR_MUL(t, axn, prod); /* x check */
+  FR_ADD(lhs, axn, t);
+  FR_MUL(t, ax, ya);
+  FR_MUL(u, ay, xa);
+  FR_ADD(rhs, t, u);
+  FR_SUB(t, lhs, rhs);
+  FR_MUL(t, t, k[2]);
+  FR_ADD(id, id, t);
+  FR_MUL(t, ayn, prod); /* y check */
+  FR_SUB(lhs, ayn, t);
+  FR_MUL(t, ay, ya);
+  FR_MUL(u, ax, xa);
+  FR_ADD(rhs, t, u);
+  FR_SUB(t, lhs, rhs);
+  FR_MUL(t, t, k[3]);
+  FR_ADD(out, id, t);
+}
+/* variable-base addition (dusk-plonk ecc/curve_addition; zksnarks curve_addtion):
+ * (x1 y2 - x1y2') + (x1y2' + y1 x2 - x3 (1 + d_E x1y2' y1 x2)) k
+ *                 + (y1 y2 + x1 x2 - y3 (1 - d_E x1y2' y1 x2)) k^2 */
+static void var_base_terms(uint64_t* out, const uint64_t* x1, const uint64_t* x3,
+                           const uint64_t* y1, const uint64_t* y3, const uint64_t* x2,
+                           const uint64_t* y2, const uint64_t* x1y2, fr_t* k,
+                           const uint64_t* ed) {
+  fr_t xy, y1x2, y1y2, x1x2, dp, t, u, id;
+  FR_MUL(xy, x1, y2);
+  FR_SUB(xy, xy, x1y2);
+  FR_MUL(y1x2, y1, x2);
+  FR_MUL(y1y2, y1, y2);
+  FR_MUL(x1x2, x1, x2);
+  FR_MUL(dp, ed, x1y2);
+  FR_MUL(dp, dp, y1x2);
+  FR_ADD(t, x1y2, y1x2);
+  FR_MUL(u, x3, dp);
+  FR_ADD(u, u, x3);
+  FR_SUB(t, t, u);
+  FR_MUL(t, t, k[1]);
+  FR_ADD(id, xy, t);
+  FR_ADD(t, y1y2, x1x2);
+  FR_MUL(u, y3, dp);
+  FR_SUB(u, y3, u);
+  FR_SUB(t, t, u);
+  FR_MUL(t, t, k[2]);
+  FR_ADD(out, id, t);
+}
+
 /* ------------------------------------------------------------------------- circuit */
 /* selector order of plk_constraint / the composer */
 enum { S_QM, S_QL, S_QR, S_QO, S_Q4, S_QC, S_QARITH, S_QRANGE, S_QLOGIC, S_QFIXED, S_QVAR, S_COUNT };
@@ -430,7 +516,6 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   const size_t GW = 51; /* u64 words per plk_constraint: 11 selectors, 6 u32, public input */
   for (size_t i = 0; i < m; ++i) {
     const uint64_t* g = gates + GW * i;
-    if (!fr_is_zero(g + 4 * S_QFIXED) || !fr_is_zero(g + 4 * S_QVAR)) return ORC_E_UNSUPPORTED;
     const uint32_t* w = (const uint32_t*)(g + 44);
     for (int c = 0; c < 4; ++c)
       if (w[c] >= nw) return ORC_E_ARG;
@@ -508,11 +593,11 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   }
   if (vk_out) memcpy(vk_out, vk, sizeof vk);
   /* 8n coset evaluations of selectors and sigmas (key.rs:220-245) */
-  static const int sel8_src[9] = {S_QM, S_QL, S_QR, S_QO, S_Q4, S_QC, S_QARITH, S_QRANGE,
-                                  S_QLOGIC};
-  uint64_t* sel8 = fr_alloc(9 * n8);
+  static const int sel8_src[11] = {S_QM, S_QL, S_QR, S_QO, S_Q4, S_QC, S_QARITH, S_QRANGE,
+                                   S_QLOGIC, S_QFIXED, S_QVAR};
+  uint64_t* sel8 = fr_alloc(11 * n8);
   uint64_t* sig8 = fr_alloc(4 * n8);
-  for (int j = 0; j < 9; ++j) {
+  for (int j = 0; j < 11; ++j) {
     memcpy(sel8 + 4 * j * n8, qc + 4 * sel8_src[j] * n, 32 * n);
     ntt_timed(sel8 + 4 * j * n8, k + 3, 1, 1, threads, &tm[2]);
   }
@@ -523,10 +608,12 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   /* v_h over the 8n coset: (g w8^i)^n - 1 (key.rs:291) */
   uint64_t* vh = fr_alloc(n8);
   orc_vanishing(k + 3, n, vh);
-  int has_range = 0, has_logic = 0;
+  int has_range = 0, has_logic = 0, has_fixed = 0, has_var = 0;
   for (size_t i = 0; i < m; ++i) {
     has_range |= !fr_is_zero(gates + GW * i + 4 * S_QRANGE);
     has_logic |= !fr_is_zero(gates + GW * i + 4 * S_QLOGIC);
+    has_fixed |= !fr_is_zero(gates + GW * i + 4 * S_QFIXED);
+    has_var |= !fr_is_zero(gates + GW * i + 4 * S_QVAR);
   }
   tm[0] = now_ns() - t_start;
 
@@ -648,12 +735,12 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   }
   t0 = now_ns();
   tr_append_commitment(&tr, "z", zcom);
-  fr_t alpha, range_sep, logic_sep, tmpc;
+  fr_t alpha, range_sep, logic_sep, fixed_sep, var_sep;
   tr_challenge_scalar(&tr, "alpha", alpha);
   tr_challenge_scalar(&tr, "range separation challenge", range_sep);
   tr_challenge_scalar(&tr, "logic separation challenge", logic_sep);
-  tr_challenge_scalar(&tr, "fixed base separation challenge", tmpc);
-  tr_challenge_scalar(&tr, "variable base separation challenge", tmpc);
+  tr_challenge_scalar(&tr, "fixed base separation challenge", fixed_sep);
+  tr_challenge_scalar(&tr, "variable base separation challenge", var_sep);
   t_tr += now_ns() - t0;
 
   /* ---- round 3: quotient (quotient_poly.rs) */
@@ -682,6 +769,15 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
   fr_set(lk[0], FR_ONE); /* logic: 1, k, k^2, k^3, k^4 with k = logic_sep^2 */
   FR_MUL(lk[1], logic_sep, logic_sep);
   for (int j = 2; j < 5; ++j) FR_MUL(lk[j], lk[j - 1], lk[1]);
+  fr_t fk[4], vbk[3], ed;
+  fr_set(fk[0], FR_ONE); /* fixed base: 1, k, k^2, k^3 with k = sep^2 */
+  FR_MUL(fk[1], fixed_sep, fixed_sep);
+  FR_MUL(fk[2], fk[1], fk[1]);
+  FR_MUL(fk[3], fk[2], fk[1]);
+  fr_set(vbk[0], FR_ONE); /* variable base: 1, k, k^2 */
+  FR_MUL(vbk[1], var_sep, var_sep);
+  FR_MUL(vbk[2], vbk[1], vbk[1]);
+  edwards_d(ed);
   uint64_t* quot = fr_alloc(n8);
   {
     const uint64_t tq = now_ns();
@@ -742,6 +838,23 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
         FR_MUL(sum, sum, sel8 + 4 * (8 * n8 + i));
         FR_MUL(sum, sum, logic_sep);
         FR_ADD(acc, acc, sum);
+      }
+      if (has_fixed) {
+        fr_t w;
+        fixed_base_terms(w, a, ev[1] + 4 * (i + 8), b, ev[2] + 4 * (i + 8), c, d, ev[4] + 4 * (i + 8),
+                         sel8 + 4 * (1 * n8 + i), sel8 + 4 * (2 * n8 + i), sel8 + 4 * (5 * n8 + i),
+                         fk, ed);
+        FR_MUL(w, w, sel8 + 4 * (9 * n8 + i));
+        FR_MUL(w, w, fixed_sep);
+        FR_ADD(acc, acc, w);
+      }
+      if (has_var) {
+        fr_t w;
+        var_base_terms(w, a, ev[1] + 4 * (i + 8), b, ev[2] + 4 * (i + 8), c, d, ev[4] + 4 * (i + 8),
+                       vbk, ed);
+        FR_MUL(w, w, sel8 + 4 * (10 * n8 + i));
+        FR_MUL(w, w, var_sep);
+        FR_ADD(acc, acc, w);
       }
       fr_set(t1 + 4 * i, acc);
     }
@@ -869,6 +982,18 @@ int orc_prove(const uint64_t* gates, size_t m, const uint64_t* witness, size_t n
       logic_terms(sum, a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, qc_e, lk);
       FR_MUL(sum, sum, logic_sep);
       poly_axpy(rc, qc + 4 * S_QLOGIC * n, n, sum);
+    }
+    if (has_fixed) {
+      fr_t w;
+      fixed_base_terms(w, a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, ql_e, qr_e, qc_e, fk, ed);
+      FR_MUL(w, w, fixed_sep);
+      poly_axpy(rc, qc + 4 * S_QFIXED * n, n, w);
+    }
+    if (has_var) {
+      fr_t w;
+      var_base_terms(w, a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, vbk, ed);
+      FR_MUL(w, w, var_sep);
+      poly_axpy(rc, qc + 4 * S_QVAR * n, n, w);
     }
     /* identity: z(X) (a + b z + g)(b + b K1 z + g)(c + b K2 z + g)(d + b K3 z + g) alpha */
     fr_t bz, idc;

@@ -131,10 +131,67 @@ def logic(a, b, bits, xor, wrong=False):
     return f
 
 
+def readme_circuit(a, b, c, d, e, f=None):
+    """README.md:28-70 TestCircuit: a + b = c (public), a < 2^6, b < 2^5, a * b = d
+    (public), e * G = f (public point) via component_mul_generator."""
+    def fn(cs):
+        from dusk_plonk_amd.prover import (JUBJUB_GENERATOR, Constraint, jubjub_mul)
+        ff = f if f is not None else jubjub_mul(JUBJUB_GENERATOR, e)
+        wa, wb = cs.append_witness(a), cs.append_witness(b)
+        cs.append_gate(Constraint().left(1).right(1).public(-c).a(wa).b(wb))
+        cs.component_range(wa, 1 << 6)
+        cs.component_range(wb, 1 << 5)
+        cs.append_gate(Constraint().mult(1).public(-d).a(wa).b(wb))
+        we = cs.append_witness(e)
+        p = cs.component_mul_generator(we, JUBJUB_GENERATOR)
+        cs.assert_equal_public_point(p, ff)
+    return fn
+
+
+def mul_generator(a, wrong=False):
+    """tests/ecc.rs:20-60: component_mul_generator(a) == append_point(a G)."""
+    def fn(cs):
+        from dusk_plonk_amd.prover import JUBJUB_GENERATOR, jubjub_mul
+        b = jubjub_mul(JUBJUB_GENERATOR, a + (1 if wrong else 0))
+        wa, wb = cs.append_witness(a), cs.append_point(b)
+        cs.assert_equal_point(cs.component_mul_generator(wa, JUBJUB_GENERATOR), wb)
+    return fn
+
+
+def add_point(a, b, wrong=False):
+    """tests/ecc.rs:111-160: component_add_point(aG, bG) == (a + b) G."""
+    def fn(cs):
+        from dusk_plonk_amd.prover import JUBJUB_GENERATOR, jubjub_mul
+        pa, pb = jubjub_mul(JUBJUB_GENERATOR, a), jubjub_mul(JUBJUB_GENERATOR, b)
+        pc = jubjub_mul(JUBJUB_GENERATOR, a + b + (1 if wrong else 0))
+        wa, wb, wc = cs.append_point(pa), cs.append_point(pb), cs.append_point(pc)
+        cs.assert_equal_point(cs.component_add_point(wa, wb), wc)
+    return fn
+
+
+def mul_point(a, b):
+    """tests/ecc.rs:236-285: component_mul_point(a, bG) == (a b) G (variable base)."""
+    def fn(cs):
+        from dusk_plonk_amd.prover import JUBJUB_GENERATOR, jubjub_mul
+        pb = jubjub_mul(JUBJUB_GENERATOR, b)
+        pc = jubjub_mul(pb, a)
+        wa, wb, wc = cs.append_witness(a), cs.append_point(pb), cs.append_point(pc)
+        cs.assert_equal_point(cs.component_mul_point(wa, wb), wc)
+    return fn
+
+
+JJ_A = 0x0A5B3C2D1E0F9A8B7C6D5E4F3A2B1C0D9E8F7A6B5C4D3E2F1A0B9C8D7E6F5A4
+JJ_B = 0x03F2E1D0C9B8A7968574635241302F1E0D1C2B3A49586776A5B4C3D2E1F0A1B
+
 A_RND = 0x3A5F0E29B8C1D47265E0F1A2B3C4D5E6F708192A3B4C5D6E7F8091A2B3C4D5E6
 B_RND = 0x2F1E3D4C5B6A79881726354453627180A9B8C7D6E5F40312233445566778899A
 
 CASES = [
+    ("test_circuit_default", readme_circuit(0, 0, 0, 0, 0, f=(0, 1)), 61),
+    ("test_circuit_20_5", readme_circuit(20, 5, 25, 100, 2), 62),
+    ("mul_generator", mul_generator(JJ_A), 63),
+    ("add_point", add_point(JJ_A, JJ_B), 64),
+    ("mul_point", mul_point(JJ_A, JJ_B), 65),
     ("and_254", logic(A_RND, B_RND, 254, False), 51),
     ("and_30", logic(A_RND, B_RND, 30, False), 52),
     ("and_0", logic(A_RND, B_RND, 0, False), 53),
@@ -191,9 +248,12 @@ def test_oracle_proof_verifies(plk, oracle, name, fn, seed):
                                 ranged(2**76, 76),
                                 decomposition(0x1234567890ABCDEF * 31337, 256, flip=10),
                                 logic(A_RND, B_RND, 254, False, wrong=True),
-                                logic(A_RND, B_RND, 64, True, wrong=True)],
+                                logic(A_RND, B_RND, 64, True, wrong=True),
+                                mul_generator(JJ_A, wrong=True), add_point(JJ_A, JJ_B, wrong=True),
+                                readme_circuit(20, 5, 26, 100, 2)],
                          ids=["boolean2", "range_neg", "range_2^76", "decomposition_flip",
-                              "and_wrong", "xor_wrong"])
+                              "and_wrong", "xor_wrong", "mul_generator_wrong", "add_point_wrong",
+                              "test_circuit_wrong_c"])
 def test_oracle_rejects_unsatisfied(plk, oracle, fn):
     tau_limbs, _ = tau_for(1)
     cs = build(fn)

@@ -105,8 +105,8 @@ def verify(vd, proof, public_inputs, tau: int) -> None:
     alpha = challenge_scalar(t, b"alpha")
     range_sep = challenge_scalar(t, b"range separation challenge")
     logic_sep = challenge_scalar(t, b"logic separation challenge")
-    challenge_scalar(t, b"fixed base separation challenge")
-    challenge_scalar(t, b"variable base separation challenge")
+    fixed_sep = challenge_scalar(t, b"fixed base separation challenge")
+    var_sep = challenge_scalar(t, b"variable base separation challenge")
     for lab, c in ((b"t_low", "t_low_comm"), (b"t_mid", "t_mid_comm"), (b"t_high", "t_high_comm"),
                    (b"t_4", "t_4_comm")):
         append_commitment(t, lab, C[c])
@@ -174,9 +174,28 @@ def verify(vd, proof, public_inputs, tau: int) -> None:
         lt = (delta(qa) + delta(qb) * k + delta(qd) * k ** 2 + (w - qa * qb) * k ** 3
               + xor_and * k ** 4) % r
         terms.append((vk["q_logic"], lt * logic_sep))
-    for lab in ("q_fixed_group_add", "q_variable_group_add"):
-        if vk[lab] is not None:
-            raise VerificationError(f"{lab} widget not restated")
+    ed = (-10240 * pow(10241, -1, r)) % r
+    if vk["q_fixed_group_add"] is not None:  # curve_scalar::linearize (fixed base)
+        k = fixed_sep * fixed_sep % r
+        ax, axn, ay, ayn = e.a_eval, e.a_next_eval, e.b_eval, e.b_next_eval
+        xya, acc, accn = e.c_eval, e.d_eval, e.d_next_eval
+        xb, yb, xyb = e.q_l_eval, e.q_r_eval, e.q_c_eval
+        bit = (accn - 2 * acc) % r
+        ya = (bit * bit * (yb - 1) + 1) % r
+        xa = xb * bit % r
+        prod = xya * ax * ay * ed % r
+        w = (bit * (bit - 1) * (bit + 1) + (bit * xyb - xya) * k
+             + (axn + axn * prod - (ax * ya + ay * xa)) * k ** 2
+             + (ayn - ayn * prod - (ay * ya + ax * xa)) * k ** 3) % r
+        terms.append((vk["q_fixed_group_add"], w * fixed_sep))
+    if vk["q_variable_group_add"] is not None:  # curve_addtion::linearize (variable base)
+        k = var_sep * var_sep % r
+        x1, x3, y1, y3 = e.a_eval, e.a_next_eval, e.b_eval, e.b_next_eval
+        x2, y2, x1y2 = e.c_eval, e.d_eval, e.d_next_eval
+        dp = ed * x1y2 * y1 * x2 % r
+        w = ((x1 * y2 - x1y2) + (x1y2 + y1 * x2 - (x3 + x3 * dp)) * k
+             + (y1 * y2 + x1 * x2 - (y3 - y3 * dp)) * k * k) % r
+        terms.append((vk["q_variable_group_add"], w * var_sep))
     bz = beta * z % r
     x = ((e.a_eval + bz + gamma) * (e.b_eval + K1 * bz + gamma) * (e.c_eval + K2 * bz + gamma)
          * (e.d_eval + K3 * bz + gamma) * alpha) % r
