@@ -426,10 +426,19 @@ PLK_HD Fe<C> fe_pow(const Fe<C>& a, const uint32_t* e, int words) {
   return r;
 }
 
+// a^e, square-and-multiply over the significant bits of e only
 template <class C>
 PLK_HD Fe<C> fe_pow_u64(const Fe<C>& a, uint64_t e) {
-  uint32_t w[2] = {(uint32_t)e, (uint32_t)(e >> 32)};
-  return fe_pow(a, w, 2);
+  Fe<C> r = fe_one<C>();
+  if (e == 0) return r;
+  int b = 63;
+  while (!((e >> b) & 1ull)) --b;
+  r = a;
+  for (--b; b >= 0; --b) {
+    r = fe_sqr(r);
+    if ((e >> b) & 1ull) r = fe_mul(r, a);
+  }
+  return r;
 }
 
 // Fermat inversion a^(p-2); inverse of zero is zero.

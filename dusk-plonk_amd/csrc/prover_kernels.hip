@@ -278,28 +278,45 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
 constexpr uint32_t kEvalThreads = 256, kEvalPer = 16, kEvalBlock = kEvalThreads * kEvalPer;
 
 // partial[k][blk] = sum_{j in block} c_j x^j   (poly k of the batch)
+// partial[k][blk] = sum_{j in block} c_j x^j   (poly k of the batch). Each thread runs
+// Horner over its kEvalPer coefficients relative to its own start; the 256 thread values
+// combine in an 8-level LDS tree with multipliers x^(kEvalPer 2^l); one power x^(block
+// start) per block.
 __global__ void __launch_bounds__(kEvalThreads) k_eval_partial(EvalBatch e, Fr* __restrict__ partial,
                                                                uint32_t max_blocks) {
   __shared__ Fr sh[kEvalThreads];
-  const uint32_t k = blockIdx.y;
+  __shared__ Fr xp[8];
+  const uint32_t k = blockIdx.y, tid = threadIdx.x;
   const Fr* p = e.poly[k];
   const uint64_t len = e.len[k];
   const Fr x = e.x[k];
-  const uint64_t base = (uint64_t)blockIdx.x * kEvalBlock + (uint64_t)threadIdx.x * kEvalPer;
+  const uint64_t block0 = (uint64_t)blockIdx.x * kEvalBlock;
+  if (block0 >= len) {  // whole block past this polynomial's end (uniform per block)
+    if (tid == 0) stf(&partial[(size_t)k * max_blocks + blockIdx.x], fe_zero<FrCfg>());
+    return;
+  }
+  if (tid == 0) {
+    Fr t = x;
+    for (uint32_t s = 1; s < kEvalPer; s <<= 1) t = fe_sqr(t);  // x^kEvalPer
+    for (int l = 0; l < 8; ++l) {
+      xp[l] = t;
+      t = fe_sqr(t);
+    }
+  }
+  const uint64_t base = block0 + (uint64_t)tid * kEvalPer;
   Fr acc = fe_zero<FrCfg>();
   if (base < len) {
-    // Horner over this thread's run, then scale by x^base
     const uint64_t top = base + kEvalPer < len ? base + kEvalPer : len;
     for (uint64_t j = top; j-- > base;) acc = fe_add(fe_mul(acc, x), ldf(&p[j]));
-    acc = fe_mul(acc, fe_pow_u64(x, base));
   }
-  sh[threadIdx.x] = acc;
+  sh[tid] = acc;
   __syncthreads();
-  for (uint32_t h = kEvalThreads / 2; h >= 1; h >>= 1) {
-    if (threadIdx.x < h) sh[threadIdx.x] = fe_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+  for (uint32_t l = 0, h = 1; h < kEvalThreads; ++l, h <<= 1) {
+    if ((tid & (2 * h - 1)) == 0) sh[tid] = fe_add(sh[tid], fe_mul(sh[tid + h], xp[l]));
     __syncthreads();
   }
-  if (threadIdx.x == 0) stf(&partial[(size_t)k * max_blocks + blockIdx.x], sh[0]);
+  if (tid == 0)
+    stf(&partial[(size_t)k * max_blocks + blockIdx.x], fe_mul(sh[0], fe_pow_u64(x, block0)));
 }
 
 __global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restrict__ partial,
@@ -331,15 +348,35 @@ __global__ void k_lincomb(LinComb lc, Fr* __restrict__ out, uint64_t len_out) {
 }
 
 // y_j = c_j * x^j (per-thread run of 16: one pow, then successive multiplies)
-__global__ void k_scale_powers(const Fr* __restrict__ c, uint64_t len, Fr x, uint64_t shift,
-                               Fr* __restrict__ y) {
-  const uint64_t j0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+// y_j = c_j x^(j + shift). A block covers 256 x 16 consecutive j; the per-thread start
+// powers x^(block start + shift) * (x^16)^t come from an 8-step product scan in LDS.
+__global__ void __launch_bounds__(256) k_scale_powers(const Fr* __restrict__ c, uint64_t len, Fr x,
+                                                      uint64_t shift, Fr* __restrict__ y) {
+  __shared__ Fr T[256];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t jb = (uint64_t)blockIdx.x * 256 * 16;
+  Fr v;
+  if (tid == 0) {
+    v = fe_pow_u64(x, jb + shift);
+  } else {
+    v = x;
+    for (int s = 0; s < 4; ++s) v = fe_sqr(v);  // x^16
+  }
+  T[tid] = v;
+  __syncthreads();
+  for (uint32_t h = 1; h < 256; h <<= 1) {  // inclusive product scan
+    const Fr o = tid >= h ? T[tid - h] : fe_one<FrCfg>();
+    __syncthreads();
+    if (tid >= h) T[tid] = fe_mul(T[tid], o);
+    __syncthreads();
+  }
+  const uint64_t j0 = jb + (uint64_t)tid * 16;
   if (j0 >= len) return;
-  Fr p = fe_pow_u64(x, j0 + shift);
+  Fr pw = T[tid];
   const uint64_t j1 = j0 + 16 < len ? j0 + 16 : len;
   for (uint64_t j = j0; j < j1; ++j) {
-    stf(&y[j], fe_mul(ldf(&c[j]), p));
-    p = fe_mul(p, x);
+    stf(&y[j], fe_mul(ldf(&c[j]), pw));
+    pw = fe_mul(pw, x);
   }
 }
 
