@@ -428,6 +428,23 @@ int plk_g1_sum(const plk_g1* points, size_t n, plk_g1* out) {
   PLK_API_END
 }
 
+int plk_srs_msm_stats_reset(plk_srs* s) {
+  if (!s) return PLK_E_ARG;
+  s->cum_accumulate_ms = 0.0;
+  s->cum_launches = s->cum_point_adds = s->cum_points = 0;
+  return PLK_OK;
+}
+
+int plk_srs_cum_msm_stats(const plk_srs* s, double* accumulate_ms, uint64_t* launches,
+                          uint64_t* point_adds, uint64_t* points) {
+  if (!s) return PLK_E_ARG;
+  if (accumulate_ms) *accumulate_ms = s->cum_accumulate_ms;
+  if (launches) *launches = s->cum_launches;
+  if (point_adds) *point_adds = s->cum_point_adds;
+  if (points) *points = s->cum_points;
+  return PLK_OK;
+}
+
 int plk_srs_last_msm_stats(const plk_srs* s, float* accumulate_ms, uint64_t* point_adds,
                            uint32_t* window_bits) {
   if (!s) return PLK_E_ARG;

@@ -111,6 +111,10 @@ struct plk_srs {
   float last_accumulate_ms = 0.f;
   uint64_t last_point_adds = 0;
   uint32_t last_slots = 0;
+  // cumulative since plk_srs_msm_stats_reset: k_accumulate time (HIP events on the MSM's
+  // stream), launches, point additions and MSM points (sum of scalar counts)
+  double cum_accumulate_ms = 0.0;
+  uint64_t cum_launches = 0, cum_point_adds = 0, cum_points = 0;
   plk_srs();
   ~plk_srs();
 };

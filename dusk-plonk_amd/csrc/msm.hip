@@ -448,6 +448,10 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
   s->last_point_adds = 0;
   for (uint32_t k = 0; k < slots; ++k) s->last_point_adds += ent[k];
   s->last_slots = slots;
+  s->cum_accumulate_ms += s->last_accumulate_ms;
+  s->cum_launches += 1;
+  s->cum_point_adds += s->last_point_adds;
+  for (uint32_t k = 0; k < slots; ++k) s->cum_points += batch.len[k];
 
   int overall = PLK_OK;
   for (uint32_t k = 0; k < slots; ++k) {

@@ -711,6 +711,15 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     TRY(key->sigma8.alloc(4 * n8 * sizeof(Fr)));
     for (int c = 0; c < 4; ++c)
       TRY(ntt_run(key->dom8, sc + c * n, key->sigma8.as<Fr>() + c * n8, n, 1, 1, nullptr, s, 1));
+    // L1 over the 8n coset, shared by every proof: idft(e_0) = n^-1 in every coefficient
+    TRY(key->l1_8n.alloc(n8 * sizeof(Fr)));
+    {
+      DevBuf tmp;
+      TRY(tmp.alloc(n * sizeof(Fr)));
+      TRY(pk_fill(tmp.as<Fr>(), key->dom->n_inv, n, s));
+      TRY(ntt_run(key->dom8, tmp.as<Fr>(), key->l1_8n.as<Fr>(), n, 1, 1, nullptr, s, 1));
+      PLK_HIP_TRY(stream_wait(s));
+    }
     // v_h[i] = (g w8^i)^n - 1 has period 8: invert the 8 values once
     const Fr gn = fe_pow_u64(key->dom8->g, n), wn = fe_pow_u64(key->dom8->omega, n);
     Fr x = gn;
@@ -774,7 +783,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     TRY(key->scan_tmp.alloc((pk_scan_tmp_elems(5 * n) + 1) * sizeof(Fr)));
     TRY(key->pi_lag.alloc(n * sizeof(Fr)));
     TRY(key->pi_coef.alloc(n * sizeof(Fr)));
-    TRY(key->ev8.alloc(7 * n8 * sizeof(Fr)));
+    TRY(key->ev8.alloc(6 * n8 * sizeof(Fr)));
     TRY(key->quot8.alloc(n8 * sizeof(Fr)));
     TRY(key->t_coef.alloc(n8 * sizeof(Fr)));
     TRY(key->r_coef.alloc(S * sizeof(Fr)));
@@ -872,7 +881,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     const Fr fixed_sep = tr.challenge_scalar("fixed base separation challenge");
     const Fr var_sep = tr.challenge_scalar("variable base separation challenge");
     Fr* pil = key->pi_lag.as<Fr>();
-    PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
+    if (!pis.empty()) PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
     // pin_small: [0, #pi) PI values uploaded here, [#pi, #pi + 16) the evaluations read
     // back in round 4 (sized once: queued copies keep pointing into it)
     TRY(key->pin_small.alloc((pis.size() + 16) * sizeof(Fr)));
@@ -881,23 +890,22 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       PLK_HIP_TRY(hipMemcpyAsync(pil + pis[i].first, key->pin_small.as<Fr>() + i, sizeof(Fr),
                                  hipMemcpyHostToDevice, s));
     }
-    TRY(ntt_run(key->dom, pil, key->pi_coef.as<Fr>(), n, -1, 0, nullptr, s, 1));
-    Fr* ev = key->ev8.as<Fr>();  // z, a, b, c, d, pi, l1*alpha^2 over the 8n coset
+    Fr* ev = key->ev8.as<Fr>();  // z, a, b, c, d, pi over the 8n coset
+    if (!pis.empty()) TRY(ntt_run(key->dom, pil, key->pi_coef.as<Fr>(), n, -1, 0, nullptr, s, 1));
     TRY(ntt_run(key->dom8, zc, ev + 0 * n8, n + 3, 1, 1, nullptr, s, 1));
     for (int c = 0; c < 4; ++c) TRY(ntt_run(key->dom8, wc + c * S, ev + (1 + c) * n8, n + 2, 1, 1, nullptr, s, 1));
-    TRY(ntt_run(key->dom8, key->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nullptr, s, 1));
-    // L1 * alpha^2 = idft(alpha^2 e_0) = alpha^2 / n in every coefficient (quotient_poly.rs:264-272)
+    // PI(X) over the coset; a circuit without public inputs has PI = 0 (the term is skipped)
+    if (!pis.empty()) TRY(ntt_run(key->dom8, key->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nullptr, s, 1));
     const Fr alpha2 = fe_sqr(alpha);
-    TRY(pk_fill(key->tmp_a.as<Fr>(), fe_mul(alpha2, key->dom->n_inv), n, s));
-    TRY(ntt_run(key->dom8, key->tmp_a.as<Fr>(), ev + 6 * n8, n, 1, 1, nullptr, s, 1));
     QuotientArgs qa{};
     qa.z = ev;
     qa.a = ev + n8;
     qa.b = ev + 2 * n8;
     qa.c = ev + 3 * n8;
     qa.d = ev + 4 * n8;
-    qa.pi = ev + 5 * n8;
-    qa.l1a = ev + 6 * n8;
+    qa.pi = pis.empty() ? nullptr : ev + 5 * n8;
+    qa.l1 = key->l1_8n.as<Fr>();
+    qa.alpha2 = alpha2;
     qa.sel = key->sel8.as<Fr>();
     qa.sigma = key->sigma8.as<Fr>();
     qa.elements8 = key->dom8->tw_fwd.as<Fr>();

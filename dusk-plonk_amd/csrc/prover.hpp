@@ -21,10 +21,10 @@ enum { SEL_QM = 0, SEL_QL, SEL_QR, SEL_QO, SEL_Q4, SEL_QC, SEL_QARITH, SEL_QRANG
        SEL_QFIXED, SEL_QVAR, SEL_COUNT8 };
 
 struct QuotientArgs {
-  const Fr *a, *b, *c, *d, *z, *pi, *l1a, *sel, *sigma, *elements8;
+  const Fr *a, *b, *c, *d, *z, *pi, *l1, *sel, *sigma, *elements8;  // pi null: no public inputs
   Fr* out;
   uint64_t n8;
-  Fr g, alpha, beta, gamma, k1, k2, k3;
+  Fr g, alpha, alpha2, beta, gamma, k1, k2, k3;
   Fr range_sep, kappa, kappa2, kappa3;
   Fr logic_sep, lk, lk2, lk3, lk4;  // logic separation challenge and its kappa powers
   Fr fixed_sep, fk, fk2, fk3;        // fixed-base scalar mul: sep, kappa = sep^2, ^2, ^3
@@ -183,6 +183,7 @@ struct plk_key {
   plk::DevBuf sigma_coef;   // 4 x n
   plk::DevBuf sigma_lag;    // 4 x n Lagrange values (= dft of sigma_coef, cached)
   plk::DevBuf sigma8;       // 4 x 8n
+  plk::DevBuf l1_8n;        // L1 over the 8n coset: coset_dft(idft(e_0)) (quotient_poly.rs:264-272)
   plk::DevBuf wire_idx;     // 4 x n witness indices per gate (u32)
   plk::Fr vh_inv[8];
   plk_g1 comms[15];         // q_m q_l q_r q_o q_c q_4 q_arith q_range q_logic q_fixed q_var s1..s4

@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
   t = fe_add(t, fe_mul(ldf(&q.sel[SEL_Q4 * N + i]), d));
   t = fe_add(t, ldf(&q.sel[SEL_QC * N + i]));
   t = fe_mul(t, ldf(&q.sel[SEL_QARITH * N + i]));
-  t = fe_add(t, ldf(&q.pi[i]));
+  if (q.pi) t = fe_add(t, ldf(&q.pi[i]));
   // range widget: sep * q_range * (D(c-4d) + D(b-4c) k + D(a-4b) k^2 + D(d_next-4a) k^3)
   if (q.has_range) {
     const Fr qr = ldf(&q.sel[SEL_QRANGE * N + i]);
@@ -270,7 +270,9 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
   cp = fe_mul(cp, fe_add(fe_add(d, fe_mul(q.beta, ldf(&q.sigma[3 * N + i]))), q.gamma));
   cp = fe_mul(cp, z_next);
   Fr perm = fe_mul(fe_sub(id, cp), q.alpha);
-  perm = fe_add(perm, fe_mul(fe_sub(z, fe_one<FrCfg>()), ldf(&q.l1a[i])));
+  // alpha^2 L1(X): coset_dft is linear, so alpha^2 * coset_dft(idft(e_0)) equals the
+  // reference's coset_dft(idft(alpha^2 e_0)) exactly
+  perm = fe_add(perm, fe_mul(fe_sub(z, fe_one<FrCfg>()), fe_mul(q.alpha2, ldf(&q.l1[i]))));
   stf(&q.out[i], fe_mul(fe_add(t, perm), q.vh_inv[i & 7]));
 }
 

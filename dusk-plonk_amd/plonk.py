@@ -39,7 +39,7 @@ ABI_SYMBOLS = (
     "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
     "plk_srs_last_msm_stats", "plk_debug_field_op", "plk_commit_batch_dev",
-    "plk_srs_setup_range", "plk_g1_sum",
+    "plk_srs_setup_range", "plk_g1_sum", "plk_srs_msm_stats_reset", "plk_srs_cum_msm_stats",
     # prover (dusk-plonk_amd/prover.py binds these)
     "plk_composer_create", "plk_composer_destroy", "plk_composer_size",
     "plk_composer_append_witness", "plk_composer_witness_value", "plk_composer_set_witness",
@@ -108,6 +108,9 @@ def _lib():
             "plk_commit_batch_dev": (i32, [vp, vp, vp, sz, vp, vp, vp]),
             "plk_srs_setup_range": (i32, [vp, vp, u64, sz, vp, pp]),
             "plk_g1_sum": (i32, [vp, sz, vp]),
+            "plk_srs_msm_stats_reset": (i32, [vp]),
+            "plk_srs_cum_msm_stats": (i32, [vp, C.POINTER(C.c_double), C.POINTER(u64),
+                                            C.POINTER(u64), C.POINTER(u64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -412,6 +415,16 @@ class PlonkParams:
             raise PlonkError(st, "commit_batch_dev")
         return [Commitment(outs[i]) if sts[i] == PLK_OK else PlonkError(sts[i], "commit")
                 for i in range(k)]
+
+    def msm_stats_reset(self):
+        _check(_lib().plk_srs_msm_stats_reset(self._h), "plk_srs_msm_stats_reset")
+
+    def cum_msm_stats(self):
+        """(accumulate ms, launches, point adds, MSM points) since msm_stats_reset."""
+        ms, ln, adds, pts = C.c_double(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(_lib().plk_srs_cum_msm_stats(self._h, C.byref(ms), C.byref(ln), C.byref(adds),
+                                            C.byref(pts)), "plk_srs_cum_msm_stats")
+        return ms.value, ln.value, adds.value, pts.value
 
     def last_msm_stats(self):
         ms, adds, c = C.c_float(), C.c_uint64(), C.c_uint32()

@@ -142,6 +142,12 @@ int plk_g1_sum(const plk_g1* points, size_t n, plk_g1* out);
  * number of bucket-accumulation point additions it performed. */
 int plk_srs_last_msm_stats(const plk_srs* srs, float* accumulate_ms, uint64_t* point_adds,
                            uint32_t* window_bits);
+/* Cumulative accumulation statistics since the last reset (measurement only): summed
+ * k_accumulate time (HIP events on the MSM's stream), launches, point additions and MSM
+ * points (scalar counts over all slots). */
+int plk_srs_msm_stats_reset(plk_srs* srs);
+int plk_srs_cum_msm_stats(const plk_srs* srs, double* accumulate_ms, uint64_t* launches,
+                          uint64_t* point_adds, uint64_t* points);
 
 /* ---- prover: Plonk composer, PlonkKey::compile, Prover::create_proof --------------------
  * The callers of the hot path, restated on the C++ host with every O(n) step
