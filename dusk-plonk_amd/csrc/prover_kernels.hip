@@ -181,6 +181,10 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_apply(const Fr* __restric
 }
 
 // ------------------------------------------------------------------------ quotient
+// Arithmetic, PI, range and permutation terms; FINAL: times 1/v_h and done, else the
+// numerator is stored for k_quotient_ext (circuits with logic / curve gates). Keeping those
+// widgets out of this kernel holds it at full occupancy (inlined, they need 256 VGPRs).
+template <bool FINAL>
 __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t N = q.n8;
@@ -215,6 +219,36 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
       t = fe_add(t, fe_mul(fe_mul(r, qr), q.range_sep));
     }
   }
+  // permutation: alpha [ z (a + bX + g)(b + bK1X + g)(c + bK2X + g)(d + bK3X + g)
+  //                    - z_next (a + b s1 + g)(b + b s2 + g)(c + b s3 + g)(d + b s4 + g) ]
+  //              + (z - 1) L1(X) alpha^2
+  const Fr X = fe_mul(q.g, ldf(&q.elements8[i]));
+  const Fr bX = fe_mul(q.beta, X);
+  Fr id = fe_mul(fe_add(fe_add(a, bX), q.gamma), fe_add(fe_add(b, fe_mul(q.k1, bX)), q.gamma));
+  id = fe_mul(id, fe_add(fe_add(c, fe_mul(q.k2, bX)), q.gamma));
+  id = fe_mul(id, fe_add(fe_add(d, fe_mul(q.k3, bX)), q.gamma));
+  id = fe_mul(id, z);
+  Fr cp = fe_add(fe_add(a, fe_mul(q.beta, ldf(&q.sigma[0 * N + i]))), q.gamma);
+  cp = fe_mul(cp, fe_add(fe_add(b, fe_mul(q.beta, ldf(&q.sigma[1 * N + i]))), q.gamma));
+  cp = fe_mul(cp, fe_add(fe_add(c, fe_mul(q.beta, ldf(&q.sigma[2 * N + i]))), q.gamma));
+  cp = fe_mul(cp, fe_add(fe_add(d, fe_mul(q.beta, ldf(&q.sigma[3 * N + i]))), q.gamma));
+  cp = fe_mul(cp, z_next);
+  Fr perm = fe_mul(fe_sub(id, cp), q.alpha);
+  // alpha^2 L1(X): coset_dft is linear, so alpha^2 * coset_dft(idft(e_0)) equals the
+  // reference's coset_dft(idft(alpha^2 e_0)) exactly
+  perm = fe_add(perm, fe_mul(fe_sub(z, fe_one<FrCfg>()), fe_mul(q.alpha2, ldf(&q.l1[i]))));
+  const Fr num = fe_add(t, perm);
+  stf(&q.out[i], FINAL ? fe_mul(num, q.vh_inv[i & 7]) : num);
+}
+
+// out[i] = (out[i] + logic + fixed-base + variable-base terms) / v_h
+__global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t N = q.n8;
+  if (i >= N) return;
+  const uint64_t nx = (i + 8) & (N - 1);
+  const Fr a = ldf(&q.a[i]), b = ldf(&q.b[i]), c = ldf(&q.c[i]), d = ldf(&q.d[i]);
+  Fr t = ldf(&q.out[i]);
   // logic widget (dusk-plonk logic gate; zksnarks, un-vendored): quads a = a_next - 4a,
   // b = b_next - 4b, d = d_next - 4d, w = c; sep q_logic (D(a) + D(b) k + D(d) k^2 +
   // (w - ab) k^3 + xor_and(a, b, w, d, q_c) k^4), k = sep^2
@@ -255,25 +289,7 @@ __global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
       t = fe_add(t, fe_mul(fe_mul(w, qv), q.var_sep));
     }
   }
-  // permutation: alpha [ z (a + bX + g)(b + bK1X + g)(c + bK2X + g)(d + bK3X + g)
-  //                    - z_next (a + b s1 + g)(b + b s2 + g)(c + b s3 + g)(d + b s4 + g) ]
-  //              + (z - 1) L1(X) alpha^2
-  const Fr X = fe_mul(q.g, ldf(&q.elements8[i]));
-  const Fr bX = fe_mul(q.beta, X);
-  Fr id = fe_mul(fe_add(fe_add(a, bX), q.gamma), fe_add(fe_add(b, fe_mul(q.k1, bX)), q.gamma));
-  id = fe_mul(id, fe_add(fe_add(c, fe_mul(q.k2, bX)), q.gamma));
-  id = fe_mul(id, fe_add(fe_add(d, fe_mul(q.k3, bX)), q.gamma));
-  id = fe_mul(id, z);
-  Fr cp = fe_add(fe_add(a, fe_mul(q.beta, ldf(&q.sigma[0 * N + i]))), q.gamma);
-  cp = fe_mul(cp, fe_add(fe_add(b, fe_mul(q.beta, ldf(&q.sigma[1 * N + i]))), q.gamma));
-  cp = fe_mul(cp, fe_add(fe_add(c, fe_mul(q.beta, ldf(&q.sigma[2 * N + i]))), q.gamma));
-  cp = fe_mul(cp, fe_add(fe_add(d, fe_mul(q.beta, ldf(&q.sigma[3 * N + i]))), q.gamma));
-  cp = fe_mul(cp, z_next);
-  Fr perm = fe_mul(fe_sub(id, cp), q.alpha);
-  // alpha^2 L1(X): coset_dft is linear, so alpha^2 * coset_dft(idft(e_0)) equals the
-  // reference's coset_dft(idft(alpha^2 e_0)) exactly
-  perm = fe_add(perm, fe_mul(fe_sub(z, fe_one<FrCfg>()), fe_mul(q.alpha2, ldf(&q.l1[i]))));
-  stf(&q.out[i], fe_mul(fe_add(t, perm), q.vh_inv[i & 7]));
+  stf(&q.out[i], fe_mul(t, q.vh_inv[i & 7]));
 }
 
 // -------------------------------------------------------------------- evaluation
@@ -452,7 +468,13 @@ int pk_scan(const Fr* in, Fr* out, uint64_t n, bool mul, bool suffix, bool exclu
 }
 
 int pk_quotient(const QuotientArgs& q, hipStream_t s) {
-  hipLaunchKernelGGL(k_quotient, dim3(blocks_for(q.n8, 256)), dim3(256), 0, s, q);
+  const dim3 grid(blocks_for(q.n8, 256));
+  if (q.has_logic || q.has_fixed || q.has_var) {
+    hipLaunchKernelGGL((k_quotient<false>), grid, dim3(256), 0, s, q);
+    hipLaunchKernelGGL(k_quotient_ext, grid, dim3(256), 0, s, q);
+  } else {
+    hipLaunchKernelGGL((k_quotient<true>), grid, dim3(256), 0, s, q);
+  }
   PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
 }
