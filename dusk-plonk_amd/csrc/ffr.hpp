@@ -220,6 +220,24 @@ PLK_RX Rx<C> rx_sub(const Rx<C>& a, const Rx<C>& b) {
   return d;
 }
 
+// a - b + 2p in (0, 4p) without the conditional pass: for operands headed straight into
+// rx_mul, which accepts inputs below 8p (Fr: 8r^2 / R' + r < 2r)
+template <class C>
+PLK_RX Rx<C> rx_sub_lazy(const Rx<C>& a, const Rx<C>& b) {
+  constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  constexpr RxConst<C> K = RxK<C>::k;
+  Rx<C> d;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int32_t t = (int32_t)(a.v[i] + K.p2[i]) - (int32_t)b.v[i] + c;
+    d.v[i] = (uint32_t)t & MASK;
+    c = t >> B;  // arithmetic: -1, 0 or +1
+  }
+  return d;
+}
+
 template <class C>
 PLK_RX Rx<C> rx_dbl(const Rx<C>& a) {
   return rx_add(a, a);

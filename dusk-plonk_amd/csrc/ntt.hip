@@ -109,19 +109,48 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   }
   __syncthreads();
 
-  // R-point DIF (natural in, bit-reversed out) on each of the T columns
-  for (int lh = (int)lr - 1; lh >= 0; --lh) {
-    const uint32_t h = 1u << lh;
+  // R-point DIF (natural in, bit-reversed out) on each of the T columns, two radix-2 stages
+  // per LDS round trip: a thread loads x0..x3 = rows j, j+h, j+2h, j+3h, applies the stage
+  // of half 2h (pairs x0/x2, x1/x3) and the stage of half h (pairs y0/y1, y2/y3) in
+  // registers, and stores once. Same butterflies and twiddles as stage-by-stage radix 2.
+  int lh = (int)lr - 1;
+  for (; lh >= 1; lh -= 2) {
+    const uint32_t h = 1u << (lh - 1);
+    const uint32_t sh1 = lr - 1 - lh, sh2 = lr - lh;  // twiddle index shifts of both stages
+    for (uint32_t g = tid; g < (E >> 2); g += bd) {
+      const uint32_t t = g & (T - 1), jg = g >> lt;
+      const uint32_t r = jg & (h - 1);
+      const uint32_t j = ((jg >> (lh - 1)) << (lh + 1)) + r;
+      const uint32_t i0 = (j << lt) + t, i1 = ((j + h) << lt) + t;
+      const uint32_t i2 = ((j + 2 * h) << lt) + t, i3 = ((j + 3 * h) << lt) + t;
+      const RFr x0 = lds_ld(data, E, i0), x1 = lds_ld(data, E, i1);
+      const RFr x2 = lds_ld(data, E, i2), x3 = lds_ld(data, E, i3);
+      // stage of half 2h: twiddle w^(r s1) for x0/x2 (identity when r = 0), w^((r+h) s1)
+      const RFr y0 = rx_add(x0, x2), y1 = rx_add(x1, x3);
+      const RFr y2 = r != 0 ? rx_mul(rx_sub_lazy(x0, x2), lds_ld(twl, H, r << sh1)) : rx_sub(x0, x2);
+      const RFr y3 = rx_mul(rx_sub_lazy(x1, x3), lds_ld(twl, H, (r + h) << sh1));
+      // stage of half h: twiddle w^(r s2) for both pairs
+      lds_st(data, E, i0, rx_add(y0, y1));
+      lds_st(data, E, i2, rx_add(y2, y3));
+      if (r != 0) {
+        const RFr w = lds_ld(twl, H, r << sh2);
+        lds_st(data, E, i1, rx_mul(rx_sub_lazy(y0, y1), w));
+        lds_st(data, E, i3, rx_mul(rx_sub_lazy(y2, y3), w));
+      } else {
+        lds_st(data, E, i1, rx_sub(y0, y1));
+        lds_st(data, E, i3, rx_sub(y2, y3));
+      }
+    }
+    __syncthreads();
+  }
+  if (lh == 0) {  // odd radix: last stage of half 1 (twiddle-free)
     for (uint32_t b = tid; b < (E >> 1); b += bd) {
       const uint32_t t = b & (T - 1), jb = b >> lt;
-      const uint32_t r = jb & (h - 1);
-      const uint32_t j1 = ((jb >> lh) << (lh + 1)) + r, j2 = j1 + h;
+      const uint32_t j1 = jb << 1;
       const RFr a = lds_ld(data, E, (j1 << lt) + t);
-      const RFr c = lds_ld(data, E, (j2 << lt) + t);
+      const RFr c = lds_ld(data, E, ((j1 + 1) << lt) + t);
       lds_st(data, E, (j1 << lt) + t, rx_add(a, c));
-      RFr d = rx_sub(a, c);
-      if (r != 0) d = rx_mul(d, lds_ld(twl, H, r << (lr - 1 - lh)));
-      lds_st(data, E, (j2 << lt) + t, d);
+      lds_st(data, E, ((j1 + 1) << lt) + t, rx_sub(a, c));
     }
     __syncthreads();
   }
