@@ -84,6 +84,39 @@ template <class C>
 struct RxK {
   static constexpr RxConst<C> k = rx_make<C>();
 };
+// c*p as L limbs (c < 16). borrow_free: every limb below the top raised by 2^B - 1 (2^B for
+// limb 0) by borrowing from the limb above, so limbs 0..L-2 lie in [2^B - 1, 2^(B+1) - 1):
+// a_i + q_i - b_i >= 0 limb by limb for any normalised b whose top limb is below q's.
+template <class C>
+struct RxMultiple {
+  uint32_t v[RxShape<C>::L];
+};
+
+template <class C>
+constexpr RxMultiple<C> rx_multiple(uint32_t c, bool borrow_free) {
+  constexpr int L = RxShape<C>::L, B = RxShape<C>::B, N = C::N;
+  uint32_t w[N + 1] = {};
+  uint64_t carry = 0;
+  for (int i = 0; i < N; ++i) {
+    const uint64_t t = (uint64_t)C::P[i] * c + carry;
+    w[i] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  w[N] = (uint32_t)carry;
+  RxMultiple<C> m{};
+  for (int i = 0; i < L; ++i) m.v[i] = rx_limb_of(w, N + 1, i, B, L);
+  if (borrow_free) {
+    m.v[0] += 1u << B;
+    for (int i = 1; i < L - 1; ++i) m.v[i] += (1u << B) - 1;
+    m.v[L - 1] -= 1;
+  }
+  return m;
+}
+
+template <class C, uint32_t CP, bool BF>
+struct RxMultipleK {
+  static constexpr RxMultiple<C> k = rx_multiple<C>(CP, BF);
+};
 
 #define PLK_RX __device__ __forceinline__
 
@@ -246,6 +279,79 @@ PLK_RX Rx<C> rx_dbl(const Rx<C>& a) {
 template <class C>
 PLK_RX Rx<C> rx_neg(const Rx<C>& a) {
   return rx_sub(rx_zero<C>(), a);
+}
+
+// ---- unnormalised differences (feed multiplications only) ---------------------------
+// a + c*p - b limb by limb, no carries: a normalised with value < 2p, b normalised with
+// value < (c - 1) p. Limbs < 2^(B+2) and value < (c + 2) p — rx_mul / rx_sqr accept such
+// operands (Fp: a 64-bit column of 14 products below 2^60 plus 14 reduction products below
+// 2^56 stays under 2^64; the output (12p)^2 / R' + p < 2p, normalised).
+template <class C, uint32_t CP>
+PLK_RX Rx<C> rx_sub_u(const Rx<C>& a, const Rx<C>& b) {
+  constexpr RxMultiple<C> Q = RxMultipleK<C, CP, true>::k;
+  Rx<C> r;
+#pragma unroll
+  for (int i = 0; i < RxShape<C>::L; ++i) r.v[i] = a.v[i] + Q.v[i] - b.v[i];
+  return r;
+}
+
+// a + c*p - b with the carries propagated (signed): normalised limbs, value in
+// (c*p - max b, c*p + max a) — no conditional pass
+template <class C, uint32_t CP>
+PLK_RX Rx<C> rx_sub_n(const Rx<C>& a, const Rx<C>& b) {
+  constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  constexpr RxMultiple<C> Q = RxMultipleK<C, CP, false>::k;
+  Rx<C> d;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int32_t t = (int32_t)(a.v[i] + Q.v[i]) - (int32_t)b.v[i] + c;
+    d.v[i] = i == L - 1 ? (uint32_t)t : ((uint32_t)t & MASK);
+    c = t >> B;
+  }
+  return d;
+}
+
+// a + c*p - b - 2e, carries propagated (the X3 of the XYZZ addition in one pass)
+template <class C, uint32_t CP>
+PLK_RX Rx<C> rx_sub2_n(const Rx<C>& a, const Rx<C>& b, const Rx<C>& e) {
+  constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  constexpr RxMultiple<C> Q = RxMultipleK<C, CP, false>::k;
+  Rx<C> d;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int32_t t =
+        (int32_t)(a.v[i] + Q.v[i]) - (int32_t)b.v[i] - (int32_t)(e.v[i] << 1) + c;
+    d.v[i] = i == L - 1 ? (uint32_t)t : ((uint32_t)t & MASK);
+    c = t >> B;
+  }
+  return d;
+}
+
+// Necessary condition for a - b == k*p with k in [-kneg, kpos] (a, b normalised): the low
+// limbs then satisfy (a0 - b0) * (-p^-1) == -k (mod 2^B). False positives ~ (kpos+kneg+1)/2^B.
+template <class C>
+PLK_RX bool rx_maybe_multiple(uint32_t a0, uint32_t b0, uint32_t kpos, uint32_t kneg) {
+  constexpr uint32_t MASK = (1u << RxShape<C>::B) - 1;
+  constexpr RxConst<C> K = RxK<C>::k;
+  return (((a0 - b0) * K.inv + kpos) & MASK) <= kpos + kneg;
+}
+
+// a (any value < 16p, limbs < 2^(B+2)) reduced to [0, 2p), normalised: a * R' / R'
+template <class C>
+PLK_RX Rx<C> rx_canon(const Rx<C>& a) {
+  return rx_mul(a, rx_one<C>());
+}
+
+// a == 0 mod p for a value < 16p with limbs < 2^(B+2): (a / R') is in [0, 2p)
+template <class C>
+PLK_RX bool rx_is_zero_u(const Rx<C>& a) {
+  Rx<C> one = rx_zero<C>();
+  one.v[0] = 1;
+  return rx_is_zero(rx_mul(a, one));
 }
 
 // a in [0, 2p): a == 0 mod p  <=>  a in {0, p}

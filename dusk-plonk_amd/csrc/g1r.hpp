@@ -26,6 +26,12 @@ __device__ __forceinline__ G1R g1r_infinity() {
 
 __device__ __forceinline__ bool g1r_is_inf(const G1R& p) { return rx_is_zero(p.ZZ); }
 
+__device__ __forceinline__ G1R g1r_neg(const G1R& p) {
+  G1R r = p;
+  r.Y = rx_neg(p.Y);
+  return r;
+}
+
 __device__ __forceinline__ G1R g1r_dbl(const G1R& p) {
   if (g1r_is_inf(p)) return p;
   const RFp U = rx_dbl(p.Y);
@@ -107,6 +113,53 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
   r.Y = rx_sub(rx_mul(R, rx_sub(Q, r.X)), rx_mul(S1, PPP));
   r.ZZ = rx_mul(rx_mul(p.ZZ, q.ZZ), PP);
   r.ZZZ = rx_mul(rx_mul(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+// ---- lazy mixed addition for the bucket accumulation (k_accumulate) ----------------
+// Same formulas as g1r_add_affine with the normalisation deferred. Accumulator invariant:
+// X in (0, 8p), Y in (0, 4p), ZZ, ZZZ in [0, 2p), all limbs normalised; g1r_lazy_finish
+// brings X, Y back to [0, 2p). The affine y may be an unnormalised value < 4p (a lazy
+// negation 4p - y). Of the seven add/sub passes of the plain formula (~125 instructions
+// each) the four that feed multiplications are limb-wise (28), X3 = R^2 - PPP - 2Q is one
+// signed-carry pass, and the P == 0 / R == 0 tests are a low-limb filter with an exact
+// check on the (rare) hits.
+__device__ __forceinline__ G1R g1r_madd_lazy(const G1R& p, const RFp& x2, const RFp& y2) {
+  if (g1r_is_inf(p)) {
+    G1R r;
+    r.X = x2;
+    r.Y = rx_canon(y2);
+    r.ZZ = rx_one<FpCfg>();
+    r.ZZZ = rx_one<FpCfg>();
+    return r;
+  }
+  const RFp U2 = rx_mul(x2, p.ZZ);
+  const RFp S2 = rx_mul(y2, p.ZZZ);
+  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);  // (2p, 12p): U2 - X1 in (-8p, 2p)
+  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);   // (2p, 8p): S2 - Y1 in (-4p, 2p)
+  if (rx_maybe_multiple<FpCfg>(U2.v[0], p.X.v[0], 1, 7) && rx_is_zero_u(P)) {
+    if (rx_maybe_multiple<FpCfg>(S2.v[0], p.Y.v[0], 1, 3) && rx_is_zero_u(R))
+      return g1r_dbl_affine(x2, rx_canon(y2));
+    return g1r_infinity();
+  }
+  const RFp PP = rx_sqr(P);
+  const RFp PPP = rx_mul(P, PP);
+  const RFp Q = rx_mul(p.X, PP);
+  G1R r;
+  r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
+  r.Y = rx_sub_n<FpCfg, 2>(rx_mul(R, rx_sub_u<FpCfg, 10>(Q, r.X)), rx_mul(p.Y, PPP));
+  r.ZZ = rx_mul(p.ZZ, PP);
+  r.ZZZ = rx_mul(p.ZZZ, PPP);
+  return r;
+}
+
+// 4p - y, unnormalised (limbs < 2^(B+1) + 2^B): the negated affine y for g1r_madd_lazy
+__device__ __forceinline__ RFp rx_neg_lazy(const RFp& y) { return rx_sub_u<FpCfg, 4>(rx_zero<FpCfg>(), y); }
+
+__device__ __forceinline__ G1R g1r_lazy_finish(const G1R& p) {
+  G1R r = p;
+  r.X = rx_canon(p.X);
+  r.Y = rx_canon(p.Y);
   return r;
 }
 

@@ -222,10 +222,10 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
       ld_aff(&table[code & 0x7fffffffu], px, py);
     }
     if (HAS_INF && table_inf[cur & 0x7fffffffu]) continue;
-    if (cur & 0x80000000u) y = rx_neg(y);
-    acc = g1r_add_affine(acc, x, y);
+    if (cur & 0x80000000u) y = rx_neg_lazy(y);
+    acc = g1r_madd_lazy(acc, x, y);
   }
-  st_g1r(&partials[(size_t)slot * task_stride + t], acc);
+  st_g1r(&partials[(size_t)slot * task_stride + t], g1r_lazy_finish(acc));
 }
 
 __global__ void __launch_bounds__(128) k_bucket_reduce(const uint32_t* __restrict__ task_off,

@@ -75,6 +75,22 @@ def test_msm_vs_oracle(plk, gpu_ctx, oracle, logn):
     assert np.array_equal(pp.commit(plk.Coefficients(sc[:m])).words, oracle.msm(pts[:m], sc[:m]))
 
 
+@pytest.mark.parametrize("tau", [1, P.R_MOD - 1])
+def test_msm_repeated_points(plk, gpu_ctx, oracle, tau):
+    """tau = 1 makes every SRS point G, tau = -1 alternates G and -G: buckets then receive
+    the same point (the accumulation's doubling branch) and a point with its negation (the
+    infinity branch) — the exceptional cases of the XYZZ mixed addition."""
+    n = 1 << 10
+    pp = plk.PlonkParams.setup(10, fr_int(tau)[0], gpu_ctx, n_points=n)
+    pts = pp.points()
+    sc = random_fr(n, seed=77)
+    few = np.tile(random_fr(3, seed=78), (n // 3 + 1, 1))[:n].copy()
+    cases = {"random": sc, "all_same": np.tile(sc[:1], (n, 1)), "three_values": few,
+             "all_one": np.tile(fr_int(1), (n, 1))}
+    for name, s in cases.items():
+        assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), name
+
+
 def test_srs_with_infinity_points(plk, gpu_ctx, oracle):
     n = 300
     pp0 = plk.PlonkParams.setup(8, random_fr(1, seed=5)[0], gpu_ctx, n_points=n)

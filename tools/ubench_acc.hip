@@ -6,6 +6,10 @@
 //   v1: software-pipelined: the next index and point are loaded before the current madd
 //   v2: v0 with a 3-waves/SIMD register budget
 //   v3: v1 with a 3-waves/SIMD register budget
+//   v4: v1 with the lazy mixed addition (g1r_madd_lazy); compared with v0 mod p
+//   (a v5 with a two-chain multiply — column k+1's products in a second accumulator — ran
+//   5% slower than v4: v_mad_u64_u32's dependent latency equals its issue cost, see
+//   tools/ubench_mad.hip)
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/ubench_acc.hip -o tools/ubench_acc
 #include <hip/hip_runtime.h>
 
@@ -76,6 +80,32 @@ __device__ __forceinline__ void acc_pipe(const uint2 task, const uint32_t* __res
   st_g1r(out, acc);
 }
 
+__device__ __forceinline__ void acc_lazy(const uint2 task, const uint32_t* __restrict__ sorted,
+                                         const G1Affine* __restrict__ table, G1xyzz* out) {
+  G1R acc = g1r_infinity();
+  const uint32_t end = task.x + task.y;
+  uint32_t code = sorted[task.x];
+  Fp px, py;
+  {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(&table[code & 0x7fffffffu]);
+    ld_fp(q, px);
+    ld_fp(q + 12, py);
+  }
+  for (uint32_t e = task.x; e < end; ++e) {
+    const RFp x = rx_unpack(px);
+    RFp y = rx_unpack(py);
+    if (code & 0x80000000u) y = rx_neg_lazy(y);
+    if (e + 1 < end) {
+      code = sorted[e + 1];
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(&table[code & 0x7fffffffu]);
+      ld_fp(q, px);
+      ld_fp(q + 12, py);
+    }
+    acc = g1r_madd_lazy(acc, x, y);
+  }
+  st_g1r(out, g1r_lazy_finish(acc));
+}
+
 __global__ void __launch_bounds__(256) k_v0(const uint2* tasks, uint32_t ntasks,
                                             const uint32_t* sorted, const G1Affine* table,
                                             G1xyzz* out) {
@@ -99,6 +129,32 @@ k_v3(const uint2* tasks, uint32_t ntasks, const uint32_t* sorted, const G1Affine
      G1xyzz* out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < ntasks) acc_pipe(tasks[t], sorted, table, &out[t]);
+}
+
+__global__ void __launch_bounds__(256) k_v4(const uint2* tasks, uint32_t ntasks,
+                                            const uint32_t* sorted, const G1Affine* table,
+                                            G1xyzz* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ntasks) acc_lazy(tasks[t], sorted, table, &out[t]);
+}
+
+// a, b in [0, 2p) as 12 words: equal mod p
+static bool eq_mod_p(const uint32_t* a, const uint32_t* b) {
+  if (!memcmp(a, b, 48)) return true;
+  uint32_t d[12];
+  uint64_t br = 0;
+  const uint32_t *hi = a, *lo = b;
+  for (int i = 11; i >= 0; --i)
+    if (a[i] != b[i]) {
+      if (a[i] < b[i]) hi = b, lo = a;
+      break;
+    }
+  for (int i = 0; i < 12; ++i) {
+    const uint64_t t = (uint64_t)hi[i] - lo[i] - br;
+    d[i] = (uint32_t)t;
+    br = (t >> 63) & 1;
+  }
+  return !memcmp(d, FpCfg::P, 48);
 }
 
 static uint64_t g_s = 0x9e37;
@@ -141,10 +197,10 @@ int main() {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  void (*ks[4])(const uint2*, uint32_t, const uint32_t*, const G1Affine*, G1xyzz*) = {k_v0, k_v1, k_v2, k_v3};
-  const char* names[4] = {"v0_plain", "v1_pipelined", "v2_plain_w3", "v3_pipelined_w3"};
+  void (*ks[5])(const uint2*, uint32_t, const uint32_t*, const G1Affine*, G1xyzz*) = {k_v0, k_v1, k_v2, k_v3, k_v4};
+  const char* names[5] = {"v0_plain", "v1_pipelined", "v2_plain_w3", "v3_pipelined_w3", "v4_lazy"};
   std::vector<G1xyzz> ref(ntasks), got(ntasks);
-  for (int v = 0; v < 4; ++v) {
+  for (int v = 0; v < 5; ++v) {
     const dim3 grid((ntasks + 255) / 256);
     hipLaunchKernelGGL(ks[v], grid, dim3(256), 0, 0, dtasks, ntasks, dsorted, dtab, dout);
     CHECK(hipDeviceSynchronize());
@@ -160,6 +216,14 @@ int main() {
                     hipMemcpyDeviceToHost));
     bool same = true;
     if (v) same = memcmp(ref.data(), got.data(), (size_t)ntasks * sizeof(G1xyzz)) == 0;
+    if (v >= 4) {  // projective coordinates agree mod p (both in [0, 2p))
+      same = true;
+      for (uint32_t t = 0; t < ntasks && same; ++t) {
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(&ref[t]);
+        const uint32_t* b = reinterpret_cast<const uint32_t*>(&got[t]);
+        for (int c = 0; c < 4 && same; ++c) same = eq_mod_p(a + 12 * c, b + 12 * c);
+      }
+    }
     std::printf("{\"test\":\"%s\",\"ms_per_msm\":%.3f,\"adds_per_s\":%.4e,\"same_as_v0\":%s}\n",
                 names[v], ms / reps, (double)entries * reps / (ms * 1e-3), same ? "true" : "false");
   }
