@@ -36,6 +36,11 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# The accumulation's own ceiling: v_mad_u64_u32 issue rate (tools/ubench_mad.hip: 3.53e13/s
+# chip-wide at 4 waves/SIMD, 3.2e13 at 2; dependent latency = issue cost) over the mads of
+# one XYZZ mixed addition in the redundant Fp form (8 mul x 392 + 2 sqr x 301, ffr.hpp).
+VALU_MAD_PEAK = 3.53e13
+MADS_PER_MIXED_ADD = 8 * 392 + 2 * 301
 
 
 def parse():
@@ -269,6 +274,14 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
     }
 
 
+def valu_roofline(adds_per_s):
+    """k_accumulate against its binding ceiling: v_mad_u64_u32 issue (mads/s)."""
+    achieved = adds_per_s * MADS_PER_MIXED_ADD
+    return {"bound": "valu (v_mad_u64_u32 issue)", "achieved": achieved, "peak": VALU_MAD_PEAK,
+            "unit": "mad/s", "frac": achieved / VALU_MAD_PEAK,
+            "mads_per_point_add": MADS_PER_MIXED_ADD}
+
+
 def load_pmc_traffic(kernel_substr: str, key: str = "hbm_bytes_per_launch"):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, made by tools/gpu_pmc.sh + tools/pmc_summary.py from the
@@ -371,6 +384,7 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": ms,
             "launches": launches, "point_adds_per_launch": adds / launches,
             "point_adds_per_s": adds / (acc_ms * 1e-3),
+            "valu": valu_roofline(adds / (acc_ms * 1e-3)),
             "note": "integer-VALU-bound (no MFMA); HBM reported as the required secondary "
                     "roofline; averages over the timed region's launches of all lanes "
                     "(4 commit batches per proof: 4, 1, 4 and 2 MSMs)",
@@ -488,6 +502,7 @@ def main():
         adds = sum(hp.msm_adds) / len(hp.msm_adds)
         result["roofline"]["point_adds_per_launch"] = adds
         result["roofline"]["point_adds_per_s"] = adds / (launch_ms * 1e-3)
+        result["roofline"]["valu"] = valu_roofline(adds / (launch_ms * 1e-3))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(k, hp.pp, threads)
