@@ -121,27 +121,22 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
 // X in (0, 8p), Y in (0, 4p), ZZ, ZZZ in [0, 2p), all limbs normalised; g1r_lazy_finish
 // brings X, Y back to [0, 2p). The affine y may be an unnormalised value < 4p (a lazy
 // negation 4p - y). Of the seven add/sub passes of the plain formula (~125 instructions
-// each) the four that feed multiplications are limb-wise (28), X3 = R^2 - PPP - 2Q is one
-// signed-carry pass, and the P == 0 / R == 0 tests are a low-limb filter with an exact
-// check on the (rare) hits.
-__device__ __forceinline__ G1R g1r_madd_lazy(const G1R& p, const RFp& x2, const RFp& y2) {
-  if (g1r_is_inf(p)) {
-    G1R r;
-    r.X = x2;
-    r.Y = rx_canon(y2);
-    r.ZZ = rx_one<FpCfg>();
-    r.ZZZ = rx_one<FpCfg>();
-    return r;
-  }
+// each) the four that feed multiplications are limb-wise (28) and X3 = R^2 - PPP - 2Q is
+// one signed-carry pass.
+//
+// g1r_madd_lazy_sl is straight-line: no exceptional-case branch. A branch in the middle
+// of the formula cost ~800 instructions per addition (the backend's per-block lowering
+// then treats operands crossing it as 64-bit: +260 mads, +540 v_mov), so the cases are
+// repaired AFTER, from the result alone:
+//   * accumulator at infinity (ZZ1 = 0): ZZ3 = ZZ1 * PP = 0;
+//   * P == 0 (same x): ZZ3 = ZZ1 * P^2 == 0, and then X3 = R^2 + 6p, so R == 0 (same
+//     point: the sum is a doubling) <=> X3 == 0 mod p; otherwise the sum is infinity.
+// A zero ZZ3 is the single (rare) trigger; g1r_madd_lazy_fix finishes those cases.
+__device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, const RFp& y2) {
   const RFp U2 = rx_mul(x2, p.ZZ);
   const RFp S2 = rx_mul(y2, p.ZZZ);
   const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);  // (2p, 12p): U2 - X1 in (-8p, 2p)
   const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);   // (2p, 8p): S2 - Y1 in (-4p, 2p)
-  if (rx_maybe_multiple<FpCfg>(U2.v[0], p.X.v[0], 1, 7) && rx_is_zero_u(P)) {
-    if (rx_maybe_multiple<FpCfg>(S2.v[0], p.Y.v[0], 1, 3) && rx_is_zero_u(R))
-      return g1r_dbl_affine(x2, rx_canon(y2));
-    return g1r_infinity();
-  }
   const RFp PP = rx_sqr(P);
   const RFp PPP = rx_mul(P, PP);
   const RFp Q = rx_mul(p.X, PP);
@@ -150,6 +145,30 @@ __device__ __forceinline__ G1R g1r_madd_lazy(const G1R& p, const RFp& x2, const 
   r.Y = rx_sub_n<FpCfg, 2>(rx_mul(R, rx_sub_u<FpCfg, 10>(Q, r.X)), rx_mul(p.Y, PPP));
   r.ZZ = rx_mul(p.ZZ, PP);
   r.ZZZ = rx_mul(p.ZZZ, PPP);
+  return r;
+}
+
+// The result of p + (x2, y2) when g1r_madd_lazy_sl returned r with r.ZZ == 0; was_inf =
+// p was the point at infinity. (x2, y2): the affine point, y2 normalised in [0, 2p).
+__device__ __forceinline__ G1R g1r_madd_lazy_fix(bool was_inf, const G1R& r, const RFp& x2,
+                                                 const RFp& y2) {
+  if (was_inf) {
+    G1R q;
+    q.X = x2;
+    q.Y = y2;
+    q.ZZ = rx_one<FpCfg>();
+    q.ZZZ = rx_one<FpCfg>();
+    return q;
+  }
+  if (rx_is_zero_u(r.X)) return g1r_dbl_affine(x2, y2);
+  return g1r_infinity();
+}
+
+// both halves, for callers that keep (x2, y2) live (y2 may be the lazy negation)
+__device__ __forceinline__ G1R g1r_madd_lazy(const G1R& p, const RFp& x2, const RFp& y2) {
+  const bool was_inf = g1r_is_inf(p);
+  G1R r = g1r_madd_lazy_sl(p, x2, y2);
+  if (rx_is_zero(r.ZZ)) r = g1r_madd_lazy_fix(was_inf, r, x2, rx_canon(y2));
   return r;
 }
 

@@ -206,14 +206,29 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
   const uint2 task = tasks[(size_t)slot * task_stride + t];
   sorted += (size_t)slot * sorted_stride;
   // software-pipelined: the next entry's index and point are loaded before the current
-  // mixed add, so the two dependent loads overlap the ~6k-instruction madd (+8%,
-  // tools/ubench_acc.hip)
-  G1R acc = g1r_infinity();
+  // mixed add, so the two dependent loads overlap the ~5k-instruction madd (+8%,
+  // tools/ubench_acc.hip). The first entry initialises the accumulator; exceptional
+  // additions (accumulator at infinity, equal x) show up as ZZ3 == 0 after the
+  // straight-line formula and are finished with the point reloaded (g1r.hpp).
   const uint32_t end = task.x + task.y;
-  uint32_t code = task.y ? sorted[task.x] : 0u;
+  G1R acc = g1r_infinity();
+  if (task.y == 0) {
+    st_g1r(&partials[(size_t)slot * task_stride + t], acc);
+    return;
+  }
+  {
+    const uint32_t c0 = sorted[task.x];
+    if (!HAS_INF || !table_inf[c0 & 0x7fffffffu]) {
+      ld_g1r_aff(&table[c0 & 0x7fffffffu], acc.X, acc.Y);
+      if (c0 & 0x80000000u) acc.Y = rx_neg(acc.Y);
+      acc.ZZ = rx_one<FpCfg>();
+      acc.ZZZ = rx_one<FpCfg>();
+    }
+  }
+  uint32_t code = task.x + 1 < end ? sorted[task.x + 1] : 0u;
   Fp px, py;
   ld_aff(&table[code & 0x7fffffffu], px, py);
-  for (uint32_t e = task.x; e < end; ++e) {
+  for (uint32_t e = task.x + 1; e < end; ++e) {
     const uint32_t cur = code;
     const RFp x = rx_unpack(px);
     RFp y = rx_unpack(py);
@@ -223,7 +238,15 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
     }
     if (HAS_INF && table_inf[cur & 0x7fffffffu]) continue;
     if (cur & 0x80000000u) y = rx_neg_lazy(y);
-    acc = g1r_madd_lazy(acc, x, y);
+    const bool was_inf = g1r_is_inf(acc);
+    G1R r = g1r_madd_lazy_sl(acc, x, y);
+    if (rx_is_zero(r.ZZ)) {  // rare: reload the point rather than keep it live
+      RFp xr, yr;
+      ld_g1r_aff(&table[cur & 0x7fffffffu], xr, yr);
+      if (cur & 0x80000000u) yr = rx_neg(yr);
+      r = g1r_madd_lazy_fix(was_inf, r, xr, yr);
+    }
+    acc = r;
   }
   st_g1r(&partials[(size_t)slot * task_stride + t], g1r_lazy_finish(acc));
 }

@@ -6,8 +6,11 @@
 //   v1: software-pipelined: the next index and point are loaded before the current madd
 //   v2: v0 with a 3-waves/SIMD register budget
 //   v3: v1 with a 3-waves/SIMD register budget
-//   v4: v1 with the lazy mixed addition (g1r_madd_lazy); compared with v0 mod p
-//   (a v5 with a two-chain multiply — column k+1's products in a second accumulator — ran
+//   v4: the production loop (msm.hip): lazy straight-line mixed addition with the
+//       exceptional cases repaired after (g1r_madd_lazy_sl/_fix); compared with v0 mod p
+//   (tried: ordering the products for short operand lifetimes — no change, the scheduler
+//   reorders anyway)
+//   (a variant with a two-chain multiply — column k+1's products in a second accumulator — ran
 //   5% slower than v4: v_mad_u64_u32's dependent latency equals its issue cost, see
 //   tools/ubench_mad.hip)
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/ubench_acc.hip -o tools/ubench_acc
@@ -82,26 +85,44 @@ __device__ __forceinline__ void acc_pipe(const uint2 task, const uint32_t* __res
 
 __device__ __forceinline__ void acc_lazy(const uint2 task, const uint32_t* __restrict__ sorted,
                                          const G1Affine* __restrict__ table, G1xyzz* out) {
-  G1R acc = g1r_infinity();
+  // msm.hip k_accumulate's loop: first entry initialises, straight-line lazy madd, rare
+  // ZZ3 == 0 repair with the point reloaded
   const uint32_t end = task.x + task.y;
-  uint32_t code = sorted[task.x];
+  G1R acc;
+  {
+    const uint32_t c0 = sorted[task.x];
+    ld_g1r_aff(&table[c0 & 0x7fffffffu], acc.X, acc.Y);
+    if (c0 & 0x80000000u) acc.Y = rx_neg(acc.Y);
+    acc.ZZ = rx_one<FpCfg>();
+    acc.ZZZ = rx_one<FpCfg>();
+  }
+  uint32_t code = task.x + 1 < end ? sorted[task.x + 1] : 0u;
   Fp px, py;
   {
     const uint32_t* q = reinterpret_cast<const uint32_t*>(&table[code & 0x7fffffffu]);
     ld_fp(q, px);
     ld_fp(q + 12, py);
   }
-  for (uint32_t e = task.x; e < end; ++e) {
+  for (uint32_t e = task.x + 1; e < end; ++e) {
+    const uint32_t cur = code;
     const RFp x = rx_unpack(px);
     RFp y = rx_unpack(py);
-    if (code & 0x80000000u) y = rx_neg_lazy(y);
     if (e + 1 < end) {
       code = sorted[e + 1];
       const uint32_t* q = reinterpret_cast<const uint32_t*>(&table[code & 0x7fffffffu]);
       ld_fp(q, px);
       ld_fp(q + 12, py);
     }
-    acc = g1r_madd_lazy(acc, x, y);
+    if (cur & 0x80000000u) y = rx_neg_lazy(y);
+    const bool was_inf = g1r_is_inf(acc);
+    G1R r = g1r_madd_lazy_sl(acc, x, y);
+    if (rx_is_zero(r.ZZ)) {
+      RFp xr, yr;
+      ld_g1r_aff(&table[cur & 0x7fffffffu], xr, yr);
+      if (cur & 0x80000000u) yr = rx_neg(yr);
+      r = g1r_madd_lazy_fix(was_inf, r, xr, yr);
+    }
+    acc = r;
   }
   st_g1r(out, g1r_lazy_finish(acc));
 }
