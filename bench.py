@@ -51,9 +51,11 @@ def parse():
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--lanes", type=int, default=2,
+    ap.add_argument("--lanes", type=int, default=3,
                     help="concurrent prover lanes per GPU (prove mode): independent contexts "
-                         "with their own streams, each driven by a host thread")
+                         "with their own streams, each driven by a host thread (sweep, "
+                         "tools/gpu_lanes*.sh: 2^20 17.6/20.2/20.9/20.8 M and 2^16 "
+                         "6.0/9.3/11.3/10.3/11.4 M constraints/s at 1/2/3/4(/6) lanes)")
     ap.add_argument("--mode", choices=["prove", "hotpath"], default="prove",
                     help="prove: full Prover::create_proof (synthesis + 5 rounds + openings); "
                          "hotpath: only the 19 NTTs + 11 MSMs of one proof")

@@ -8,6 +8,7 @@
 //   v3: v1 with a 3-waves/SIMD register budget
 //   v4: the production loop (msm.hip): lazy straight-line mixed addition with the
 //       exceptional cases repaired after (g1r_madd_lazy_sl/_fix); compared with v0 mod p
+//   v5: v4 with a 3-waves/SIMD register budget
 //   (tried: ordering the products for short operand lifetimes — no change, the scheduler
 //   reorders anyway)
 //   (a variant with a two-chain multiply — column k+1's products in a second accumulator — ran
@@ -158,6 +159,12 @@ __global__ void __launch_bounds__(256) k_v4(const uint2* tasks, uint32_t ntasks,
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < ntasks) acc_lazy(tasks[t], sorted, table, &out[t]);
 }
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+k_v5(const uint2* tasks, uint32_t ntasks, const uint32_t* sorted, const G1Affine* table,
+     G1xyzz* out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ntasks) acc_lazy(tasks[t], sorted, table, &out[t]);
+}
 
 // a, b in [0, 2p) as 12 words: equal mod p
 static bool eq_mod_p(const uint32_t* a, const uint32_t* b) {
@@ -218,10 +225,10 @@ int main() {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  void (*ks[5])(const uint2*, uint32_t, const uint32_t*, const G1Affine*, G1xyzz*) = {k_v0, k_v1, k_v2, k_v3, k_v4};
-  const char* names[5] = {"v0_plain", "v1_pipelined", "v2_plain_w3", "v3_pipelined_w3", "v4_lazy"};
+  void (*ks[6])(const uint2*, uint32_t, const uint32_t*, const G1Affine*, G1xyzz*) = {k_v0, k_v1, k_v2, k_v3, k_v4, k_v5};
+  const char* names[6] = {"v0_plain", "v1_pipelined", "v2_plain_w3", "v3_pipelined_w3", "v4_lazy", "v5_lazy_w3"};
   std::vector<G1xyzz> ref(ntasks), got(ntasks);
-  for (int v = 0; v < 5; ++v) {
+  for (int v = 0; v < 6; ++v) {
     const dim3 grid((ntasks + 255) / 256);
     hipLaunchKernelGGL(ks[v], grid, dim3(256), 0, 0, dtasks, ntasks, dsorted, dtab, dout);
     CHECK(hipDeviceSynchronize());
