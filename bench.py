@@ -218,6 +218,7 @@ def cpu_baseline(k: int, pp, threads: int):
     per_proof = 11 * t_msm + 11 * t_ntt + 8 * t_ntt8
     return {
         "value": n / per_proof, "unit": "constraints/s", "cores": threads, "kind": "port",
+        "host": host_info(),
         "sample": (f"oracle/plk_oracle.c (restated reference CPU path, OpenMP {threads} threads): "
                    f"1x MSM(2^{k}) {t_msm:.2f}s, 1x dft(2^{k}) {t_ntt:.3f}s, "
                    f"1x coset_dft(2^{k + 3}) {t_ntt8:.3f}s; per-proof hot path = "
@@ -264,8 +265,20 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
         orc.coset_dft(v8, k + 3, threads)
         t_ntt8 = time.perf_counter() - t0
         per_proof = 11 * t_msm + 11 * t_ntt + 8 * t_ntt8 + other_s * (n / ns)
+    # the same restated prover on ONE core, at 2^12 (seconds, not extrapolated)
+    k1 = min(k, 12)
+    cs1 = Plonk()
+    cs1.synthetic_chain((1 << k1) - 14, 78)
+    g1, w1 = cs1.export()
+    trim1 = (1 << (g1.shape[0] + 6 - 1).bit_length()) + 8
+    r1 = orc.prove(g1, w1, pp.points(0, trim1), b"cpu-baseline-1", 5, 1)
+    one_core_s = float(r1["timing_ns"][6]) / 1e9  # create_proof phase (compile excluded)
     return {
         "value": n / per_proof, "unit": "constraints/s", "cores": threads, "kind": "port",
+        "host": host_info(),
+        "single_core": {"n": 1 << k1, "seconds": one_core_s,
+                        "value": (1 << k1) / one_core_s, "unit": "constraints/s",
+                        "note": "full create_proof (key compile excluded) on 1 thread"},
         "sample": (f"oracle/plk_prover_oracle.c (restated reference CPU prover, OpenMP {threads} "
                    f"threads): one full create_proof at 2^{ks} = {prove_s:.2f} s "
                    f"({ns / prove_s:.0f} constraints/s; MSM {msm_s:.2f} s, NTT {ntt_s:.2f} s, "
@@ -274,6 +287,23 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
                    f"11 x dft(2^{k}) {t_ntt:.3f} s + 8 x coset_dft(2^{k + 3}) {t_ntt8:.3f} s + "
                    f"O(n) phases x {n // ns} = {per_proof:.1f} s"),
     }
+
+
+def host_info():
+    """nproc, usable cores and the CPU model of the machine the baseline ran on."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"nproc": os.cpu_count(), "usable_cores": usable, "cpu_model": model}
 
 
 def valu_roofline(adds_per_s):
