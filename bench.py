@@ -376,6 +376,19 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
         m_, l_, a_, p_ = lane.pp.cum_msm_stats()
         acc_ms, launches, adds, points = acc_ms + m_, launches + l_, adds + a_, points + p_
     cbits = fp.pp.last_msm_stats()[2]
+    # the same kernel with the GPU to itself: one more proof on lane 0 after the timed
+    # region (the in-workload figure above shares the chip with the other lanes' kernels)
+    solo = None
+    if L > 1:
+        fp.pp.msm_stats_reset()
+        fp.step(timed=False)
+        torch.cuda.synchronize()
+        s_ms, s_l, s_a, s_p = fp.pp.cum_msm_stats()
+        if s_l and s_ms > 0:
+            solo = {"avg_launch_ms": s_ms / s_l, "launches": s_l,
+                    "point_adds_per_s": s_a / (s_ms * 1e-3),
+                    "valu": valu_roofline(s_a / (s_ms * 1e-3)),
+                    "note": "one proof with no other lane running (outside the timed region)"}
     result = {
         "metric": "PLONK prover constraints/sec (BLS12-381) at n=2^16 and 2^20, 1/2/4/8 GPUs",
         "value": n * steps * L * world / elapsed,
@@ -417,6 +430,7 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
             "launches": launches, "point_adds_per_launch": adds / launches,
             "point_adds_per_s": adds / (acc_ms * 1e-3),
             "valu": valu_roofline(adds / (acc_ms * 1e-3)),
+            "solo": solo,
             "note": "integer-VALU-bound (no MFMA); HBM reported as the required secondary "
                     "roofline; averages over the timed region's launches of all lanes "
                     "(4 commit batches per proof: 4, 1, 4 and 2 MSMs)",

@@ -946,6 +946,10 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     // split into t_low, t_mid, t_high (n each) and t_4 = t[3n..] (prover.rs:252-265)
     plk_g1 tcom[4];
     TRY(key_commit(key, {tc, tc + n, tc + 2 * n, tc + 3 * n}, {n, n, n, 5 * n}, tcom, nullptr, s));
+    // t_4 is 5n coefficients in the reference (prover.rs:259); its commit succeeded, so
+    // everything past the committed SRS prefix is zero (key_commit checks the tail): t and
+    // t_4 end at 3n + t4_len for the evaluation and the opening below
+    const uint64_t t4_len = std::min<uint64_t>(5 * n, std::min<uint64_t>(key->srs->n, key->n_trim));
     tr.append_commitment("t_low", tcom[0]);
     tr.append_commitment("t_mid", tcom[1]);
     tr.append_commitment("t_high", tcom[2]);
@@ -960,14 +964,14 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     const Fr* polys[16] = {tc, wc, wc + S, wc + 2 * S, wc + 3 * S, sc, sc + n, sc + 2 * n,
                            qc + QARITH * n, qc + QC * n, qc + QL * n, qc + QR * n,
                            wc, wc + S, wc + 3 * S, zc};
-    const uint64_t lens[16] = {n8, n + 2, n + 2, n + 2, n + 2, n, n, n, n, n, n, n,
+    const uint64_t lens[16] = {3 * n + t4_len, n + 2, n + 2, n + 2, n + 2, n, n, n, n, n, n, n,
                                n + 2, n + 2, n + 2, n + 3};
     for (int i = 0; i < 16; ++i) {
       eb.poly[i] = polys[i];
       eb.len[i] = lens[i];
       eb.x[i] = i < 12 ? zeta : zw;
     }
-    TRY(pk_eval(eb, 16, n8, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
+    TRY(pk_eval(eb, 16, 3 * n + t4_len, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
     Fr evs[16];
     Fr* evs_pin = key->pin_small.as<Fr>() + pis.size();
     PLK_HIP_TRY(hipMemcpyAsync(evs_pin, key->eval_out.ptr, sizeof evs, hipMemcpyDeviceToHost, s));
@@ -1049,7 +1053,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     er.poly[0] = rc;
     er.len[0] = n + 3;
     er.x[0] = zeta;
-    TRY(pk_eval(er, 1, n8, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
+    TRY(pk_eval(er, 1, n + 3, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
     const Fr r_e = d2h_fr(key->eval_out.as<Fr>(), s);
 
     const char* elabels[17] = {"a_eval", "b_eval", "c_eval", "d_eval", "a_next_eval",
@@ -1073,10 +1077,13 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       la.s[la.terms] = sc_;
       ++la.terms;
     };
+    // the aggregate and its quotient by (X - z) stop where t_4 does (same polynomials,
+    // same commits)
+    const uint64_t agg_len = std::max<uint64_t>(n + 3, t4_len);
     lt(tc, n, one);
     lt(tc + n, n, zn);
     lt(tc + 2 * n, n, z2n);
-    lt(tc + 3 * n, 5 * n, z3n);
+    lt(tc + 3 * n, t4_len, z3n);
     Fr vp = v1;
     lt(rc, n + 3, vp);
     for (int c = 0; c < 4; ++c) {
@@ -1088,10 +1095,10 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       lt(sc + c * n, n, vp);
     }
     Fr* ag = key->agg.as<Fr>();
-    TRY(pk_lincomb(la, ag, 5 * n, s));
+    TRY(pk_lincomb(la, ag, agg_len, s));
     Fr* w1 = key->w_coef.as<Fr>();
     Fr* w2 = w1 + 5 * n;
-    TRY(pk_ruffini(ag, 5 * n, zeta, w1, key->tmp_a.as<Fr>(), st, s));
+    TRY(pk_ruffini(ag, agg_len, zeta, w1, key->tmp_a.as<Fr>(), st, s));
     // W'(X) = (z + v2 a + v2^2 b + v2^3 d) / (X - z w)
     LinComb lb{};
     lb.terms = 4;
@@ -1111,7 +1118,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     TRY(pk_lincomb(lb, ag2, n + 3, s));
     TRY(pk_ruffini(ag2, n + 3, zw, w2, key->tmp_a.as<Fr>(), st, s));
     plk_g1 wcm[2];
-    TRY(key_commit(key, {w1, w2}, {5 * n - 1, n + 2}, wcm, nullptr, s));
+    TRY(key_commit(key, {w1, w2}, {agg_len - 1, n + 2}, wcm, nullptr, s));
 
     // ---- proof (proof.rs:36-66)
     proof->a_comm = wcom[0];

@@ -295,15 +295,28 @@ __global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
 // -------------------------------------------------------------------- evaluation
 constexpr uint32_t kEvalThreads = 256, kEvalPer = 16, kEvalBlock = kEvalThreads * kEvalPer;
 
-// partial[k][blk] = sum_{j in block} c_j x^j   (poly k of the batch)
-// partial[k][blk] = sum_{j in block} c_j x^j   (poly k of the batch). Each thread runs
-// Horner over its kEvalPer coefficients relative to its own start; the 256 thread values
-// combine in an 8-level LDS tree with multipliers x^(kEvalPer 2^l); one power x^(block
-// start) per block.
+// x^(b * 4096) from x4096 = x^4096 by square-and-multiply over the bits of b: at most
+// 2 log2(b) multiplies, where fe_pow_u64(x, b * 4096) would chain ~1.5 * log2(b * 4096)
+// of them (~380 at n = 2^23, run by one thread while its workgroup waits)
+__device__ __forceinline__ Fr pow_blocks(Fr x4096, uint64_t b) {
+  Fr r = fe_one<FrCfg>();
+  for (; b; b >>= 1) {
+    if (b & 1) r = fe_mul(r, x4096);
+    x4096 = fe_sqr(x4096);
+  }
+  return r;
+}
+
+// partial[k][blk] = sum_{j in block} c_j x^j (poly k of the batch). Thread t runs Horner
+// in x^256 over c_{block + t + 256 i}, i < kEvalPer (consecutive threads read consecutive
+// coefficients: coalesced), giving H_t with sum_j c_j x^j = sum_t x^t H_t; the workgroup
+// folds that by halving (H_t += x^h H_{t+h}, h = 128 .. 1) with x^h from 8 squarings; one
+// power x^(block start) per block (pow_blocks).
 __global__ void __launch_bounds__(kEvalThreads) k_eval_partial(EvalBatch e, Fr* __restrict__ partial,
                                                                uint32_t max_blocks) {
   __shared__ Fr sh[kEvalThreads];
-  __shared__ Fr xp[8];
+  __shared__ Fr xp[9];  // x^(2^l), l = 0..8 (x^256 last)
+  __shared__ Fr xblock;
   const uint32_t k = blockIdx.y, tid = threadIdx.x;
   const Fr* p = e.poly[k];
   const uint64_t len = e.len[k];
@@ -315,26 +328,30 @@ __global__ void __launch_bounds__(kEvalThreads) k_eval_partial(EvalBatch e, Fr* 
   }
   if (tid == 0) {
     Fr t = x;
-    for (uint32_t s = 1; s < kEvalPer; s <<= 1) t = fe_sqr(t);  // x^kEvalPer
-    for (int l = 0; l < 8; ++l) {
+    for (int l = 0; l < 9; ++l) {
       xp[l] = t;
       t = fe_sqr(t);
     }
+    for (int l = 9; l < 12; ++l) t = fe_sqr(t);  // x^4096
+    xblock = pow_blocks(t, blockIdx.x);
   }
-  const uint64_t base = block0 + (uint64_t)tid * kEvalPer;
+  __syncthreads();
+  const Fr x256 = xp[8];
   Fr acc = fe_zero<FrCfg>();
-  if (base < len) {
-    const uint64_t top = base + kEvalPer < len ? base + kEvalPer : len;
-    for (uint64_t j = top; j-- > base;) acc = fe_add(fe_mul(acc, x), ldf(&p[j]));
+#pragma unroll
+  for (int i = (int)kEvalPer - 1; i >= 0; --i) {
+    const uint64_t j = block0 + tid + (uint64_t)i * kEvalThreads;
+    acc = fe_mul(acc, x256);
+    if (j < len) acc = fe_add(acc, ldf(&p[j]));
   }
   sh[tid] = acc;
   __syncthreads();
-  for (uint32_t l = 0, h = 1; h < kEvalThreads; ++l, h <<= 1) {
-    if ((tid & (2 * h - 1)) == 0) sh[tid] = fe_add(sh[tid], fe_mul(sh[tid + h], xp[l]));
+  for (int l = 7; l >= 0; --l) {
+    const uint32_t h = 1u << l;
+    if (tid < h) sh[tid] = fe_add(sh[tid], fe_mul(sh[tid + h], xp[l]));
     __syncthreads();
   }
-  if (tid == 0)
-    stf(&partial[(size_t)k * max_blocks + blockIdx.x], fe_mul(sh[0], fe_pow_u64(x, block0)));
+  if (tid == 0) stf(&partial[(size_t)k * max_blocks + blockIdx.x], fe_mul(sh[0], xblock));
 }
 
 __global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restrict__ partial,
@@ -373,12 +390,13 @@ __global__ void __launch_bounds__(256) k_scale_powers(const Fr* __restrict__ c, 
   __shared__ Fr T[256];
   const uint32_t tid = threadIdx.x;
   const uint64_t jb = (uint64_t)blockIdx.x * 256 * 16;
-  Fr v;
-  if (tid == 0) {
-    v = fe_pow_u64(x, jb + shift);
-  } else {
-    v = x;
-    for (int s = 0; s < 4; ++s) v = fe_sqr(v);  // x^16
+  Fr v = x;
+  for (int s = 0; s < 4; ++s) v = fe_sqr(v);  // x^16
+  if (tid == 0) {  // x^(jb + shift), jb = 4096 * blockIdx.x
+    Fr x4096 = v;
+    for (int s = 0; s < 8; ++s) x4096 = fe_sqr(x4096);
+    v = pow_blocks(x4096, blockIdx.x);
+    if (shift) v = fe_mul(v, fe_pow_u64(x, shift));
   }
   T[tid] = v;
   __syncthreads();
