@@ -189,8 +189,10 @@ struct DeviceGuard {
 };
 
 int ntt_build_domain(plk_domain* d);
+// pre_table (forward coset transforms only): R'-domain multipliers for the len_in inputs
+// in place of the domain's g^j table — a scaled table (c g^j) yields the evaluations of c p
 int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset,
-            Fr* scratch, hipStream_t stream, uint32_t count);
+            Fr* scratch, hipStream_t stream, uint32_t count, const Fr* pre_table = nullptr);
 int msm_prepare_srs(plk_srs* s, hipStream_t stream);
 int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g1* out,
             hipStream_t stream);

@@ -309,7 +309,7 @@ int ntt_build_domain(plk_domain* d) {
 }
 
 int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset, Fr* scratch,
-            hipStream_t stream, uint32_t count) {
+            hipStream_t stream, uint32_t count, const Fr* pre_table) {
   const uint64_t n = d->n;
   if (len_in > n) return PLK_E_ARG;
   if (n == 1) {  // size-1 transform: identity (times n^-1 = 1, g^0 = 1)
@@ -351,7 +351,8 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
 #define PLK_LAUNCH(PRE, POST)                                                                 \
   hipLaunchKernelGGL((k_ntt_pass<PRE, POST>), grid, dim3(bd), lds, stream, src, dst, tw, ptw, \
-                     d->coset_pow.as<Fr>(), d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n,   \
+                     pre_table ? pre_table : d->coset_pow.as<Fr>(), d->icoset_scale.as<Fr>(), \
+                     n_inv_rx, d->log_n,                                                      \
                      ps.lp, ps.lr, ps.lt, lin, (uint64_t)n)
     if (pre == 0 && post == 0) PLK_LAUNCH(0, 0);
     else if (pre == 1 && post == 0) PLK_LAUNCH(1, 0);

@@ -11,6 +11,7 @@
 #include <mutex>
 #include <vector>
 
+#include "ffr.hpp"
 #include "internal.hpp"
 #include "msm_common.hpp"
 #include "prover.hpp"
@@ -720,6 +721,16 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
       TRY(ntt_run(key->dom8, tmp.as<Fr>(), key->l1_8n.as<Fr>(), n, 1, 1, nullptr, s, 1));
       PLK_HIP_TRY(stream_wait(s));
     }
+    // coset tables with 2^5 / 2^-5 folded in (k_quotient exponents, prover.hpp): the wire
+    // and public-input transforms read at most n + 3 coefficients
+    {
+      const uint64_t nt = std::min<uint64_t>(n8, n + 8);
+      TRY(key->coset_w.alloc(nt * sizeof(Fr)));
+      TRY(key->coset_pi.alloc(nt * sizeof(Fr)));
+      const Fr c32 = fr_u64(32);
+      TRY(pk_scale_copy(key->dom8->coset_pow.as<Fr>(), c32, key->coset_w.as<Fr>(), nt, s));
+      TRY(pk_scale_copy(key->dom8->coset_pow.as<Fr>(), fe_inv(c32), key->coset_pi.as<Fr>(), nt, s));
+    }
     // v_h[i] = (g w8^i)^n - 1 has period 8: invert the 8 values once
     const Fr gn = fe_pow_u64(key->dom8->g, n), wn = fe_pow_u64(key->dom8->omega, n);
     Fr x = gn;
@@ -893,9 +904,15 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     Fr* ev = key->ev8.as<Fr>();  // z, a, b, c, d, pi over the 8n coset
     if (!pis.empty()) TRY(ntt_run(key->dom, pil, key->pi_coef.as<Fr>(), n, -1, 0, nullptr, s, 1));
     TRY(ntt_run(key->dom8, zc, ev + 0 * n8, n + 3, 1, 1, nullptr, s, 1));
-    for (int c = 0; c < 4; ++c) TRY(ntt_run(key->dom8, wc + c * S, ev + (1 + c) * n8, n + 2, 1, 1, nullptr, s, 1));
+    // wire evaluations at exponent -1 and PI at +1 for k_quotient's redundant-form
+    // arithmetic (QuotientArgs): scaled coset tables, no extra pass
+    for (int c = 0; c < 4; ++c)
+      TRY(ntt_run(key->dom8, wc + c * S, ev + (1 + c) * n8, n + 2, 1, 1, nullptr, s, 1,
+                  key->coset_w.as<Fr>()));
     // PI(X) over the coset; a circuit without public inputs has PI = 0 (the term is skipped)
-    if (!pis.empty()) TRY(ntt_run(key->dom8, key->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nullptr, s, 1));
+    if (!pis.empty())
+      TRY(ntt_run(key->dom8, key->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nullptr, s, 1,
+                  key->coset_pi.as<Fr>()));
     const Fr alpha2 = fe_sqr(alpha);
     QuotientArgs qa{};
     qa.z = ev;
@@ -940,6 +957,24 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     qa.has_fixed = key->has_fixed ? 1 : 0;
     qa.has_var = key->has_var ? 1 : 0;
     for (int j = 0; j < 8; ++j) qa.vh_inv[j] = key->vh_inv[j];
+    {  // exponent-scaled constants for k_quotient (x[e] = x R 2^(-5e); [-1] = R' domain)
+      auto em1 = [](const Fr& x) { return fe_to_rx_domain(x); };
+      auto em2 = [](const Fr& x) { return fe_to_rx_domain(fe_to_rx_domain(x)); };
+      const Fr one = fe_one<FrCfg>(), two = fe_dbl(one);
+      qa.rx_bg = em2(fe_mul(beta, key->dom8->g));
+      qa.rx_beta = em2(beta);
+      qa.rx_gamma = em1(gamma);
+      qa.rx_one_w = em1(one);
+      qa.rx_two_w = em1(two);
+      qa.rx_three_w = em1(fe_add(two, one));
+      qa.rx_kappa = em1(qa.kappa);
+      qa.rx_kappa2 = em1(qa.kappa2);
+      qa.rx_kappa3 = em1(qa.kappa3);
+      qa.rx_alpha2 = em1(alpha2);
+      for (int j = 0; j < 8; ++j) qa.rx_vh[j] = em2(key->vh_inv[j]);
+      qa.rx_32 = fr_u64(32);
+      qa.rx_inv32 = fe_inv(qa.rx_32);
+    }
     TRY(pk_quotient(qa, s));
     Fr* tc = key->t_coef.as<Fr>();
     TRY(ntt_run(key->dom8, key->quot8.as<Fr>(), tc, n8, -1, 1, nullptr, s, 1));

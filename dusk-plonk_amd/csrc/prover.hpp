@@ -32,6 +32,17 @@ struct QuotientArgs {
   Fr edwards_d;                      // JubJub d = -10240/10241
   int has_range, has_logic, has_fixed, has_var;
   Fr vh_inv[8];
+  // k_quotient runs in the redundant form (ffr.hpp): a value with exponent e is stored as
+  // x R 2^(-5e) (e = 0: the R domain; e = -1: the R' domain) and rx_mul adds exponents
+  // plus one. Wire evaluations arrive at e = -1 (coset table scaled by 2^5), public
+  // inputs at e = +1, z / selectors / sigmas / L1 / elements at e = 0; these constants are
+  // pre-scaled so every term meets at e = 1 and num / v_h lands at e = 0 (the R domain).
+  Fr rx_bg, rx_beta, rx_gamma;          // beta g and beta at e = -2, gamma at e = -1
+  Fr rx_one_w, rx_two_w, rx_three_w;    // 1, 2, 3 at e = -1 (range widget deltas)
+  Fr rx_kappa, rx_kappa2, rx_kappa3;    // range kappa powers at e = -1
+  Fr rx_alpha2;                         // alpha^2 at e = -1 (alpha and range_sep at e = 0)
+  Fr rx_vh[8];                          // 1 / v_h at e = -2
+  Fr rx_inv32, rx_32;                   // 2^-5 and 2^5 (R domain): k_quotient_ext converts
 };
 
 constexpr int kMaxEval = 16;
@@ -124,6 +135,8 @@ uint64_t pk_scan_tmp_elems(uint64_t n);
 int pk_scan(const Fr* in, Fr* out, uint64_t n, bool mul, bool suffix, bool exclusive, Fr* tmp,
             hipStream_t s);
 int pk_quotient(const QuotientArgs& q, hipStream_t s);
+// out[j] = in[j] * c (packed Montgomery product), j < n
+int pk_scale_copy(const Fr* in, const Fr& c, Fr* out, uint64_t n, hipStream_t s);
 uint32_t pk_eval_max_blocks(uint64_t max_len);
 int pk_eval(const EvalBatch& e, uint32_t count, uint64_t max_len, Fr* partial, Fr* d_out,
             hipStream_t s);
@@ -184,6 +197,8 @@ struct plk_key {
   plk::DevBuf sigma_lag;    // 4 x n Lagrange values (= dft of sigma_coef, cached)
   plk::DevBuf sigma8;       // 4 x 8n
   plk::DevBuf l1_8n;        // L1 over the 8n coset: coset_dft(idft(e_0)) (quotient_poly.rs:264-272)
+  plk::DevBuf coset_w;      // 2^5 g^j (R' domain), j < n + 8: wire evaluations at e = -1
+  plk::DevBuf coset_pi;     // 2^-5 g^j (R' domain): public-input evaluations at e = +1
   plk::DevBuf wire_idx;     // 4 x n witness indices per gate (u32)
   plk::Fr vh_inv[8];
   plk_g1 comms[15];         // q_m q_l q_r q_o q_c q_4 q_arith q_range q_logic q_fixed q_var s1..s4

@@ -12,6 +12,7 @@
 //    aggregate witness numerators) and Ruffini division by (X - z)
 #include <hip/hip_runtime.h>
 
+#include "ffr.hpp"
 #include "internal.hpp"
 #include "prover.hpp"
 
@@ -33,6 +34,9 @@ __device__ __forceinline__ void stf(Fr* p, const Fr& v) {
   q[0] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
   q[1] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
 }
+
+using RFr = Rx<FrCfg>;
+__device__ __forceinline__ RFr ldr(const Fr* p) { return rx_unpack(ldf(p)); }
 
 inline uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
@@ -185,60 +189,68 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_apply(const Fr* __restric
 // numerator is stored for k_quotient_ext (circuits with logic / curve gates). Keeping those
 // widgets out of this kernel holds it at full occupancy (inlined, they need 256 VGPRs).
 template <bool FINAL>
-__global__ void __launch_bounds__(256) k_quotient(QuotientArgs q) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) k_quotient(QuotientArgs q) {
+  // Redundant-limb arithmetic (ffr.hpp) with exponent bookkeeping (QuotientArgs): [e] marks
+  // a value stored as x R 2^(-5e); rx_mul(x[e1], y[e2]) = xy[e1 + e2 + 1]; additions need
+  // equal exponents. Wires [-1], z / selectors / sigmas / L1 / elements [0].
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t N = q.n8;
   if (i >= N) return;
   const uint64_t nx = (i + 8) & (N - 1);  // "next row" of the n-domain inside the 8n domain
-  const Fr a = ldf(&q.a[i]), b = ldf(&q.b[i]), c = ldf(&q.c[i]), d = ldf(&q.d[i]);
-  const Fr z = ldf(&q.z[i]), z_next = ldf(&q.z[nx]);
-  // arithmetic widget: q_arith (q_m a b + q_l a + q_r b + q_o c + q_4 d + q_c)
-  Fr t = fe_mul(ldf(&q.sel[SEL_QM * N + i]), fe_mul(a, b));
-  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_QL * N + i]), a));
-  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_QR * N + i]), b));
-  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_QO * N + i]), c));
-  t = fe_add(t, fe_mul(ldf(&q.sel[SEL_Q4 * N + i]), d));
-  t = fe_add(t, ldf(&q.sel[SEL_QC * N + i]));
-  t = fe_mul(t, ldf(&q.sel[SEL_QARITH * N + i]));
-  if (q.pi) t = fe_add(t, ldf(&q.pi[i]));
+  const RFr a = ldr(&q.a[i]), b = ldr(&q.b[i]), c = ldr(&q.c[i]), d = ldr(&q.d[i]);
+  const RFr z = ldr(&q.z[i]), z_next = ldr(&q.z[nx]);
+  // arithmetic widget: q_arith (q_m a b + q_l a + q_r b + q_o c + q_4 d + q_c), terms [0]
+  RFr t = rx_mul(ldr(&q.sel[SEL_QM * N + i]), rx_mul(a, b));
+  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_QL * N + i]), a));
+  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_QR * N + i]), b));
+  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_QO * N + i]), c));
+  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_Q4 * N + i]), d));
+  t = rx_add(t, ldr(&q.sel[SEL_QC * N + i]));
+  t = rx_mul(t, ldr(&q.sel[SEL_QARITH * N + i]));  // [1]
+  if (q.pi) t = rx_add(t, ldr(&q.pi[i]));           // public inputs arrive at [1]
   // range widget: sep * q_range * (D(c-4d) + D(b-4c) k + D(a-4b) k^2 + D(d_next-4a) k^3)
   if (q.has_range) {
-    const Fr qr = ldf(&q.sel[SEL_QRANGE * N + i]);
-    if (!fe_is_zero(qr)) {
-      const Fr d_next = ldf(&q.d[nx]);
-      const Fr one = fe_one<FrCfg>();
-      const Fr two = fe_dbl(one), three = fe_add(two, one);
-      auto delta = [&](const Fr& f) {
-        return fe_mul(fe_mul(f, fe_sub(f, one)), fe_mul(fe_sub(f, two), fe_sub(f, three)));
+    const RFr qr = ldr(&q.sel[SEL_QRANGE * N + i]);
+    if (!rx_is_zero(qr)) {
+      const RFr d_next = ldr(&q.d[nx]);
+      const RFr one = rx_unpack(q.rx_one_w), two = rx_unpack(q.rx_two_w),
+                three = rx_unpack(q.rx_three_w);  // [-1]
+      auto delta = [&](const RFr& f) {          // [-1] -> [-1]
+        return rx_mul(rx_mul(f, rx_sub(f, one)), rx_mul(rx_sub(f, two), rx_sub(f, three)));
       };
-      auto four = [](const Fr& x) { return fe_dbl(fe_dbl(x)); };
-      Fr r = delta(fe_sub(c, four(d)));
-      r = fe_add(r, fe_mul(delta(fe_sub(b, four(c))), q.kappa));
-      r = fe_add(r, fe_mul(delta(fe_sub(a, four(b))), q.kappa2));
-      r = fe_add(r, fe_mul(delta(fe_sub(d_next, four(a))), q.kappa3));
-      t = fe_add(t, fe_mul(fe_mul(r, qr), q.range_sep));
+      auto four = [](const RFr& x) { return rx_dbl(rx_dbl(x)); };
+      RFr r = delta(rx_sub(c, four(d)));
+      r = rx_add(r, rx_mul(delta(rx_sub(b, four(c))), rx_unpack(q.rx_kappa)));
+      r = rx_add(r, rx_mul(delta(rx_sub(a, four(b))), rx_unpack(q.rx_kappa2)));
+      r = rx_add(r, rx_mul(delta(rx_sub(d_next, four(a))), rx_unpack(q.rx_kappa3)));
+      t = rx_add(t, rx_mul(rx_mul(r, qr), rx_unpack(q.range_sep)));  // [-1] -> [0] -> [1]
     }
   }
   // permutation: alpha [ z (a + bX + g)(b + bK1X + g)(c + bK2X + g)(d + bK3X + g)
   //                    - z_next (a + b s1 + g)(b + b s2 + g)(c + b s3 + g)(d + b s4 + g) ]
   //              + (z - 1) L1(X) alpha^2
-  const Fr X = fe_mul(q.g, ldf(&q.elements8[i]));
-  const Fr bX = fe_mul(q.beta, X);
-  Fr id = fe_mul(fe_add(fe_add(a, bX), q.gamma), fe_add(fe_add(b, fe_mul(q.k1, bX)), q.gamma));
-  id = fe_mul(id, fe_add(fe_add(c, fe_mul(q.k2, bX)), q.gamma));
-  id = fe_mul(id, fe_add(fe_add(d, fe_mul(q.k3, bX)), q.gamma));
-  id = fe_mul(id, z);
-  Fr cp = fe_add(fe_add(a, fe_mul(q.beta, ldf(&q.sigma[0 * N + i]))), q.gamma);
-  cp = fe_mul(cp, fe_add(fe_add(b, fe_mul(q.beta, ldf(&q.sigma[1 * N + i]))), q.gamma));
-  cp = fe_mul(cp, fe_add(fe_add(c, fe_mul(q.beta, ldf(&q.sigma[2 * N + i]))), q.gamma));
-  cp = fe_mul(cp, fe_add(fe_add(d, fe_mul(q.beta, ldf(&q.sigma[3 * N + i]))), q.gamma));
-  cp = fe_mul(cp, z_next);
-  Fr perm = fe_mul(fe_sub(id, cp), q.alpha);
+  // K1..K3 = 7, 13, 17 (permutation.rs:28-30) by additions
+  const RFr bX = rx_mul(rx_unpack(q.rx_bg), ldr(&q.elements8[i]));  // beta g w^i [-1]
+  const RFr bX2 = rx_dbl(bX), bX4 = rx_dbl(bX2), bX8 = rx_dbl(bX4), bX16 = rx_dbl(bX8);
+  const RFr bX7 = rx_sub(bX8, bX), bX13 = rx_add(rx_add(bX8, bX4), bX), bX17 = rx_add(bX16, bX);
+  const RFr gm = rx_unpack(q.rx_gamma);  // [-1]
+  RFr id = rx_mul(rx_add(rx_add(a, bX), gm), rx_add(rx_add(b, bX7), gm));
+  id = rx_mul(id, rx_add(rx_add(c, bX13), gm));
+  id = rx_mul(id, rx_add(rx_add(d, bX17), gm));
+  id = rx_mul(id, z);  // [0]
+  const RFr be = rx_unpack(q.rx_beta);  // [-2]
+  RFr cp = rx_add(rx_add(a, rx_mul(be, ldr(&q.sigma[0 * N + i]))), gm);
+  cp = rx_mul(cp, rx_add(rx_add(b, rx_mul(be, ldr(&q.sigma[1 * N + i]))), gm));
+  cp = rx_mul(cp, rx_add(rx_add(c, rx_mul(be, ldr(&q.sigma[2 * N + i]))), gm));
+  cp = rx_mul(cp, rx_add(rx_add(d, rx_mul(be, ldr(&q.sigma[3 * N + i]))), gm));
+  cp = rx_mul(cp, z_next);  // [0]
+  RFr perm = rx_mul(rx_sub(id, cp), rx_unpack(q.alpha));  // [1]
   // alpha^2 L1(X): coset_dft is linear, so alpha^2 * coset_dft(idft(e_0)) equals the
   // reference's coset_dft(idft(alpha^2 e_0)) exactly
-  perm = fe_add(perm, fe_mul(fe_sub(z, fe_one<FrCfg>()), fe_mul(q.alpha2, ldf(&q.l1[i]))));
-  const Fr num = fe_add(t, perm);
-  stf(&q.out[i], FINAL ? fe_mul(num, q.vh_inv[i & 7]) : num);
+  const RFr zm1 = rx_sub(z, rx_unpack(fe_one<FrCfg>()));
+  perm = rx_add(perm, rx_mul(rx_mul(zm1, ldr(&q.l1[i])), rx_unpack(q.rx_alpha2)));  // [1]
+  const RFr num = rx_add(t, perm);                                                    // [1]
+  stf(&q.out[i], rx_pack_canonical(FINAL ? rx_mul(num, rx_unpack(q.rx_vh[i & 7])) : num));
 }
 
 // out[i] = (out[i] + logic + fixed-base + variable-base terms) / v_h
@@ -247,8 +259,11 @@ __global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
   const uint64_t N = q.n8;
   if (i >= N) return;
   const uint64_t nx = (i + 8) & (N - 1);
-  const Fr a = ldf(&q.a[i]), b = ldf(&q.b[i]), c = ldf(&q.c[i]), d = ldf(&q.d[i]);
-  Fr t = ldf(&q.out[i]);
+  // k_quotient left num at exponent +1 and the wire evaluations are at -1 (QuotientArgs):
+  // back to the R domain for the packed arithmetic here
+  auto ldw = [&](const Fr* p) { return fe_mul(ldf(p), q.rx_inv32); };
+  const Fr a = ldw(&q.a[i]), b = ldw(&q.b[i]), c = ldw(&q.c[i]), d = ldw(&q.d[i]);
+  Fr t = fe_mul(ldf(&q.out[i]), q.rx_32);
   // logic widget (dusk-plonk logic gate; zksnarks, un-vendored): quads a = a_next - 4a,
   // b = b_next - 4b, d = d_next - 4d, w = c; sep q_logic (D(a) + D(b) k + D(d) k^2 +
   // (w - ab) k^3 + xor_and(a, b, w, d, q_c) k^4), k = sep^2
@@ -260,9 +275,9 @@ __global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
       auto delta = [&](const Fr& f) {
         return fe_mul(fe_mul(f, fe_sub(f, one)), fe_mul(fe_sub(f, two), fe_sub(f, three)));
       };
-      const Fr qa = fe_sub(ldf(&q.a[nx]), fe_mul(four, a));
-      const Fr qb = fe_sub(ldf(&q.b[nx]), fe_mul(four, b));
-      const Fr qd = fe_sub(ldf(&q.d[nx]), fe_mul(four, d));
+      const Fr qa = fe_sub(ldw(&q.a[nx]), fe_mul(four, a));
+      const Fr qb = fe_sub(ldw(&q.b[nx]), fe_mul(four, b));
+      const Fr qd = fe_sub(ldw(&q.d[nx]), fe_mul(four, d));
       const Fr qc = ldf(&q.sel[SEL_QC * N + i]);
       Fr r = delta(qa);
       r = fe_add(r, fe_mul(delta(qb), q.lk));
@@ -275,7 +290,7 @@ __global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
   if (q.has_fixed) {
     const Fr qf = ldf(&q.sel[SEL_QFIXED * N + i]);
     if (!fe_is_zero(qf)) {
-      const Fr w = widget_fixed_base(a, ldf(&q.a[nx]), b, ldf(&q.b[nx]), c, d, ldf(&q.d[nx]),
+      const Fr w = widget_fixed_base(a, ldw(&q.a[nx]), b, ldw(&q.b[nx]), c, d, ldw(&q.d[nx]),
                                      ldf(&q.sel[SEL_QL * N + i]), ldf(&q.sel[SEL_QR * N + i]),
                                      ldf(&q.sel[SEL_QC * N + i]), q.fk, q.fk2, q.fk3, q.edwards_d);
       t = fe_add(t, fe_mul(fe_mul(w, qf), q.fixed_sep));
@@ -284,12 +299,18 @@ __global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
   if (q.has_var) {
     const Fr qv = ldf(&q.sel[SEL_QVAR * N + i]);
     if (!fe_is_zero(qv)) {
-      const Fr w = widget_var_base(a, ldf(&q.a[nx]), b, ldf(&q.b[nx]), c, d, ldf(&q.d[nx]),
+      const Fr w = widget_var_base(a, ldw(&q.a[nx]), b, ldw(&q.b[nx]), c, d, ldw(&q.d[nx]),
                                    q.vk, q.vk2, q.edwards_d);
       t = fe_add(t, fe_mul(fe_mul(w, qv), q.var_sep));
     }
   }
   stf(&q.out[i], fe_mul(t, q.vh_inv[i & 7]));
+}
+
+// ------------------------------------------------------------ scaled table copy
+__global__ void k_scale_copy(const Fr* __restrict__ in, Fr c, Fr* __restrict__ out, uint64_t n) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) stf(&out[j], fe_mul(ldf(&in[j]), c));
 }
 
 // -------------------------------------------------------------------- evaluation
@@ -499,6 +520,13 @@ int pk_quotient(const QuotientArgs& q, hipStream_t s) {
 
 uint32_t pk_eval_max_blocks(uint64_t max_len) {
   return (uint32_t)((max_len + kEvalBlock - 1) / kEvalBlock);
+}
+
+int pk_scale_copy(const Fr* in, const Fr& c, Fr* out, uint64_t n, hipStream_t s) {
+  if (n == 0) return PLK_OK;
+  hipLaunchKernelGGL(k_scale_copy, dim3(blocks_for(n, 256)), dim3(256), 0, s, in, c, out, n);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
 }
 
 int pk_eval(const EvalBatch& e, uint32_t count, uint64_t max_len, Fr* partial, Fr* d_out,
