@@ -43,7 +43,14 @@ def _compile(src: Path, obj: Path) -> str:
     return src.name
 
 
-def build(verbose: bool = True, jobs: int | None = None) -> Path:
+def build(verbose: bool = True, jobs: int | None = None, variant: str = "",
+          extra: tuple = ()) -> Path:
+    """variant / extra: an experimental build (extra hipcc flags, e.g. -DPLK_ACC_WAVES=3)
+    into build-<variant>/ and libplk-<variant>.so, loaded with PLK_LIB=<path>."""
+    global BUILD, LIB, CFLAGS
+    if variant:
+        BUILD, LIB = PKG / f"build-{variant}", PKG / f"libplk-{variant}.so"
+        CFLAGS = CFLAGS + list(extra)
     BUILD.mkdir(exist_ok=True)
     hdrs = _headers()
     srcs = sorted(CSRC.glob("*.hip"))
@@ -75,5 +82,8 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
 
 
 if __name__ == "__main__":
-    build()
+    if len(sys.argv) > 1:  # build_ext.py <variant> <extra hipcc flags...>
+        build(variant=sys.argv[1], extra=tuple(sys.argv[2:]))
+    else:
+        build()
     sys.exit(0)

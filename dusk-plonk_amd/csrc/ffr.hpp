@@ -169,6 +169,44 @@ PLK_RX Rx<C> rx_mul(const Rx<C>& a, const Rx<C>& b) {
   return r;
 }
 
+// (a*b + c*d) / R' mod p with ONE Montgomery reduction: both product columns accumulate
+// into the same 64-bit column (the caller bounds the limbs so that 2L products plus L
+// reduction products stay below 2^64, and the value so that (ab + cd) / R' + p < 2p).
+template <class C>
+PLK_RX Rx<C> rx_mul_add(const Rx<C>& a, const Rx<C>& b, const Rx<C>& c, const Rx<C>& d) {
+  constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  constexpr RxConst<C> K = RxK<C>::k;
+  uint32_t m[L];
+  Rx<C> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc += (uint64_t)c.v[i] * d.v[k - i];
+#pragma unroll
+    for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+    m[k] = ((uint32_t)acc * K.inv) & MASK;
+    acc += (uint64_t)m[k] * K.p[0];
+    acc >>= B;
+  }
+#pragma unroll
+  for (int k = L; k < 2 * L - 1; ++k) {
+#pragma unroll
+    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+#pragma unroll
+    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)c.v[i] * d.v[k - i];
+#pragma unroll
+    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+    r.v[k - L] = (uint32_t)acc & MASK;
+    acc >>= B;
+  }
+  r.v[L - 1] = (uint32_t)acc;
+  return r;
+}
+
 // a^2 / R': the cross products a_i a_j (i < j) once, doubled
 template <class C>
 PLK_RX Rx<C> rx_sqr(const Rx<C>& a) {

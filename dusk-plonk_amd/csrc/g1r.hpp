@@ -142,7 +142,10 @@ __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, con
   const RFp Q = rx_mul(p.X, PP);
   G1R r;
   r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
-  r.Y = rx_sub_n<FpCfg, 2>(rx_mul(R, rx_sub_u<FpCfg, 10>(Q, r.X)), rx_mul(p.Y, PPP));
+  // Y3 = R (Q - X3) + (5p - Y1) PPP with one reduction: limbs of R, Q - X3 + 10p below
+  // 3*2^28, of 5p - Y1 below 2^29, PPP normalised -> columns < 168 * 2^56 < 2^64; value
+  // (8p * 12p + 5p * 2p) / R' + p < 1.06p
+  r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP);
   r.ZZ = rx_mul(p.ZZ, PP);
   r.ZZZ = rx_mul(p.ZZZ, PPP);
   return r;

@@ -88,47 +88,71 @@ __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cf
 }
 
 // single workgroup per slot: offsets = exclusive scan(counts) (also the scatter cursors),
-// task_off = exclusive scan(ceil(count / CH))
+// task_off = exclusive scan(ceil(count / CH)) (where each bucket's partial sums go), and the
+// EXECUTION order of the tasks: all full tasks (CH entries) first in bucket order, then the
+// partial tails grouped by length, longest first, so that a wavefront's lanes run tasks of
+// (nearly) the same length. len_cur[slot][l] = first execution slot of the tails of length l.
 __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restrict__ counts,
                                                        uint32_t B, uint32_t chunk,
                                                        uint32_t* __restrict__ offsets,
                                                        uint32_t* __restrict__ task_off,
-                                                       uint32_t* __restrict__ cursor) {
-  __shared__ uint32_t s_cnt[1024], s_tsk[1024];
+                                                       uint32_t* __restrict__ cursor,
+                                                       uint32_t* __restrict__ full_off,
+                                                       uint32_t* __restrict__ len_cur) {
+  __shared__ uint32_t s_cnt[1024], s_tsk[1024], s_full[1024], s_len[kChunkMax];
   const uint32_t slot = blockIdx.y;
   counts += (size_t)slot * B;
   offsets += (size_t)slot * (B + 1);
   task_off += (size_t)slot * (B + 1);
   cursor += (size_t)slot * B;
+  full_off += (size_t)slot * B;
+  len_cur += (size_t)slot * kChunkMax;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  if (tid < kChunkMax) s_len[tid] = 0;
+  __syncthreads();
   const uint32_t per = (B + nt - 1) / nt;
   const uint32_t b0 = tid * per;
-  uint32_t c_sum = 0, t_sum = 0;
+  uint32_t c_sum = 0, t_sum = 0, f_sum = 0;
   for (uint32_t b = b0; b < b0 + per && b < B; ++b) {
-    c_sum += counts[b];
-    t_sum += (counts[b] + chunk - 1) / chunk;
+    const uint32_t c = counts[b];
+    c_sum += c;
+    t_sum += (c + chunk - 1) / chunk;
+    f_sum += c / chunk;
+    if (c % chunk) atomicAdd(&s_len[c % chunk], 1u);
   }
   s_cnt[tid] = c_sum;
   s_tsk[tid] = t_sum;
+  s_full[tid] = f_sum;
   __syncthreads();
   for (uint32_t off = 1; off < nt; off <<= 1) {
     uint32_t a = tid >= off ? s_cnt[tid - off] : 0, b = tid >= off ? s_tsk[tid - off] : 0;
+    uint32_t f = tid >= off ? s_full[tid - off] : 0;
     __syncthreads();
     s_cnt[tid] += a;
     s_tsk[tid] += b;
+    s_full[tid] += f;
     __syncthreads();
   }
-  uint32_t c_run = s_cnt[tid] - c_sum, t_run = s_tsk[tid] - t_sum;
+  uint32_t c_run = s_cnt[tid] - c_sum, t_run = s_tsk[tid] - t_sum, f_run = s_full[tid] - f_sum;
   for (uint32_t b = b0; b < b0 + per && b < B; ++b) {
     offsets[b] = c_run;
     cursor[b] = c_run;
     task_off[b] = t_run;
+    full_off[b] = f_run;
     c_run += counts[b];
     t_run += (counts[b] + chunk - 1) / chunk;
+    f_run += counts[b] / chunk;
   }
   if (tid == nt - 1) {
     offsets[B] = s_cnt[tid];
     task_off[B] = s_tsk[tid];
+  }
+  if (tid == 0) {  // tails after the full tasks, longest first
+    uint32_t run = s_full[nt - 1];
+    for (uint32_t l = chunk - 1; l >= 1; --l) {
+      len_cur[l] = run;
+      run += s_len[l];
+    }
   }
 }
 
@@ -173,10 +197,15 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
   }
 }
 
-// task t of bucket b covers sorted[offsets[b] + t*CH, ...+CH)
+// Task t of bucket b covers sorted[offsets[b] + t*CH, ...+CH) and writes its partial sum to
+// partials[task_off[b] + t]; its execution slot is full_off[b] + t for a full task, or the
+// next slot of its length class for the tail. tasks[slot] = {first entry, partial index |
+// (length - 1) << 26}.
 __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
-                             const uint32_t* __restrict__ task_off, uint32_t B, uint32_t chunk,
-                             uint2* __restrict__ tasks, uint64_t task_stride) {
+                             const uint32_t* __restrict__ task_off,
+                             const uint32_t* __restrict__ full_off, uint32_t* __restrict__ len_cur,
+                             uint32_t B, uint32_t chunk, uint2* __restrict__ tasks,
+                             uint64_t task_stride) {
   const uint32_t slot = blockIdx.y;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
@@ -184,15 +213,21 @@ __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
   task_off += (size_t)slot * (B + 1);
   tasks += (size_t)slot * task_stride;
   const uint32_t start = offsets[b], cnt = offsets[b + 1] - start;
-  uint32_t t = task_off[b];
-  for (uint32_t o = 0; o < cnt; o += chunk, ++t) {
-    const uint32_t l = cnt - o < chunk ? cnt - o : chunk;
-    tasks[t] = make_uint2(start + o, l);
+  const uint32_t t0 = task_off[b], nfull = cnt / chunk;
+  uint32_t x = full_off[(size_t)slot * B + b];
+  for (uint32_t t = 0; t < nfull; ++t, ++x)
+    tasks[x] = make_uint2(start + t * chunk, (t0 + t) | ((chunk - 1) << 26));
+  if (const uint32_t tail = cnt - nfull * chunk) {
+    const uint32_t e = atomicAdd(&len_cur[(size_t)slot * kChunkMax + tail], 1u);
+    tasks[e] = make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << 26));
   }
 }
 
+#ifndef PLK_ACC_WAVES
+#define PLK_ACC_WAVES 1  // min waves per SIMD requested from the register allocator
+#endif
 template <bool HAS_INF>
-__global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ tasks,
+__global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* __restrict__ tasks,
                                                     const uint32_t* __restrict__ task_off,
                                                     uint32_t B, uint64_t task_stride,
                                                     const uint32_t* __restrict__ sorted,
@@ -203,7 +238,9 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
   const uint32_t slot = blockIdx.y;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= task_off[(size_t)slot * (B + 1) + B]) return;
-  const uint2 task = tasks[(size_t)slot * task_stride + t];
+  const uint2 tk = tasks[(size_t)slot * task_stride + t];
+  const uint2 task = make_uint2(tk.x, (tk.y >> 26) + 1);  // first entry, length (>= 1)
+  const uint32_t pidx = tk.y & ((1u << 26) - 1);
   sorted += (size_t)slot * sorted_stride;
   // software-pipelined: the next entry's index and point are loaded before the current
   // mixed add, so the two dependent loads overlap the ~5k-instruction madd (+8%,
@@ -212,10 +249,6 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
   // straight-line formula and are finished with the point reloaded (g1r.hpp).
   const uint32_t end = task.x + task.y;
   G1R acc = g1r_infinity();
-  if (task.y == 0) {
-    st_g1r(&partials[(size_t)slot * task_stride + t], acc);
-    return;
-  }
   {
     const uint32_t c0 = sorted[task.x];
     if (!HAS_INF || !table_inf[c0 & 0x7fffffffu]) {
@@ -248,7 +281,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint2* __restrict__ ta
     }
     acc = r;
   }
-  st_g1r(&partials[(size_t)slot * task_stride + t], g1r_lazy_finish(acc));
+  st_g1r(&partials[(size_t)slot * task_stride + pidx], g1r_lazy_finish(acc));
 }
 
 __global__ void __launch_bounds__(128) k_bucket_reduce(const uint32_t* __restrict__ task_off,
@@ -345,11 +378,14 @@ int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
   const size_t entries = (size_t)s->windows * len;
   const size_t max_tasks = entries / kChunkMin + B + 1;
   const size_t G = (B + 255) / 256;
+  if (max_tasks >= ((size_t)1 << 26)) return PLK_E_ARG;  // task records hold 26-bit partial indices
   int st;
   if ((st = w.counts.alloc(slots * B * 4))) return st;
   if ((st = w.offsets.alloc(slots * (B + 1) * 4))) return st;
   if ((st = w.task_off.alloc(slots * (B + 1) * 4))) return st;
   if ((st = w.cursor.alloc(slots * B * 4))) return st;
+  if ((st = w.full_off.alloc(slots * B * 4))) return st;
+  if ((st = w.len_cur.alloc(slots * kChunkMax * 4))) return st;
   if ((st = w.sorted.alloc(slots * (entries + 1) * 4))) return st;
   if ((st = w.tasks.alloc(slots * max_tasks * sizeof(uint2)))) return st;
   if ((st = w.partials.alloc(slots * max_tasks * sizeof(G1xyzz)))) return st;
@@ -422,14 +458,16 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
   }
   hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
                      w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
-                     w.task_off.as<uint32_t>(), w.cursor.as<uint32_t>());
+                     w.task_off.as<uint32_t>(), w.cursor.as<uint32_t>(),
+                     w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>());
   if (max_len) {
     hipLaunchKernelGGL(k_scatter, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream,
                        batch, cfg, (uint64_t)s->n, w.cursor.as<uint32_t>(),
                        w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride);
   }
   hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
-                     w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), B, chunk,
+                     w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),
+                     w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>(), B, chunk,
                      w.tasks.as<uint2>(), (uint64_t)w.task_stride);
   PLK_HIP_TRY(hipEventRecord(w.ev0, stream));
   if (s->has_inf) {

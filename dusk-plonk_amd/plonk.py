@@ -27,7 +27,8 @@ from pathlib import Path
 import numpy as np
 
 _PKG = Path(__file__).resolve().parent
-_LIB_PATH = _PKG / "libplk.so"
+# PLK_LIB: an alternative build of the same library (tools/ A/B experiments)
+_LIB_PATH = Path(os.environ["PLK_LIB"]) if os.environ.get("PLK_LIB") else _PKG / "libplk.so"
 
 PLK_OK, PLK_E_DEGREE, PLK_E_ARG, PLK_E_DEVICE, PLK_E_OOM, PLK_E_NODEV = range(6)
 
