@@ -38,9 +38,11 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # The accumulation's own ceiling: v_mad_u64_u32 issue rate (tools/ubench_mad.hip: 3.53e13/s
 # chip-wide at 4 waves/SIMD, 3.2e13 at 2; dependent latency = issue cost) over the mads of
-# one XYZZ mixed addition in the redundant Fp form (8 mul x 392 + 2 sqr x 301, ffr.hpp).
+# one XYZZ mixed addition in the redundant Fp form (ffr.hpp / g1r.hpp): 8 products x 196 +
+# 2 squares x 105 + 9 Montgomery reductions x 196 (Y3 = R(Q - X3) - Y1 PPP is one fused
+# sum of two products) = 3542, the count of v_mad_u64_u32 in the compiled loop body.
 VALU_MAD_PEAK = 3.53e13
-MADS_PER_MIXED_ADD = 8 * 392 + 2 * 301
+MADS_PER_MIXED_ADD = 8 * 196 + 2 * 105 + 9 * 196
 
 
 def parse():

@@ -4,21 +4,23 @@
 // prover.rs:133-136,194,262-265,440,452 and key.rs:138-159).
 //
 // Design (fixed-base Pippenger, all windows folded into one bucket set):
-//  * SRS load (srs.hip): table[w][i] = 2^(c*w) * P_i in affine form, w < W = ceil(256/c),
-//    resident in HBM (W * n * 96 B: 1.6 GB at n = 2^20, c = 16). Commit bases are always
-//    an SRS prefix, so the table is built once.
-//  * Per MSM: each scalar is recoded into W signed c-bit digits |d| <= 2^(c-1); digit
-//    (i, w) sends +-table[w][i] to bucket |d|-1: ONE set of B = 2^(c-1) buckets and no
-//    per-window doubling chain.
-//  * Counting sort by bucket with a per-CU LDS histogram (B * 4 B <= 128 KiB): LDS atomics
-//    per digit, one coalesced global atomic per (workgroup, bucket) to count and again to
-//    reserve ranges. Order inside a bucket is irrelevant: group addition is exact and the
-//    canonical affine output is unique.
+//  * SRS load (srs.hip): table[w][i] = 2^(c*w) * P_i in affine form, w < W, resident in
+//    HBM (W * n * 96 B: 1.5 GB at n = 2^20, c = 17, W = 15). Commit bases are always an
+//    SRS prefix, so the table is built once.
+//  * Per MSM: each scalar s is first brought to [0, (r-1)/2] (s or r - s with the signs
+//    flipped, scalar_half), then recoded into W = ceil(255/c) signed c-bit digits
+//    |d| <= 2^(c-1); digit (i, w) sends +-table[w][i] to bucket |d|-1: ONE set of
+//    B = 2^(c-1) buckets and no per-window doubling chain.
+//  * Counting sort by bucket: per-workgroup LDS histograms (windows of 32 K buckets =
+//    128 KiB; c = 17 takes two) written whole, a per-bucket scan over the workgroups
+//    (k_block_scan) instead of global atomics, then LDS atomics place each digit. Order
+//    inside a bucket is irrelevant: group addition is exact and the canonical affine
+//    output is unique.
 //  * Bucket accumulation in chunks of CH points (one thread per chunk, XYZZ mixed adds):
 //    the dominant kernel, integer-VALU bound.
-//  * Bucket reduction sum_b (b+1) S_b = sum_j 2^j T_j with T_j = sum of the buckets whose
-//    weight has bit j set: two shallow tree kernels give the c points T_j and the CPU runs
-//    the 2c-op Horner tail and the single inversion to canonical affine.
+//  * Bucket reduction sum_b (b+1) S_b = sum_j 2^j T_j (T_j: sums of buckets selected by the
+//    bits of their weight, see k_bitsum1): two shallow tree kernels give the c points T_j and
+//    the CPU runs the 2c-op Horner tail and the single inversion to canonical affine.
 //  * Up to kMaxSlots independent MSMs run as ONE batch (blockIdx.y = slot): the prover's
 //    commits come in independent groups (4 wires, 4 quotient chunks, 2 openings), and the
 //    latency-bound tail kernels of a batch then cost about what one MSM's tail costs.
@@ -36,6 +38,7 @@ namespace plk {
 namespace {
 
 constexpr uint32_t kHistThreads = 1024;
+constexpr uint32_t kHistBlocksMax = 256;  // histogram / scatter workgroups per slot
 
 // signed c-bit digit w of canonical scalar s (carry threaded through the caller)
 __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, uint32_t c, uint32_t& carry) {
@@ -63,31 +66,75 @@ __device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t&
   i1 = min(len, i0 + per);
 }
 
-// Pass 1: LDS histogram of this workgroup's digits, flushed to counts[slot][b].
+// Canonical scalar in [0, (r-1)/2]: s, or r - s with the digit signs flipped (s P = (r - s)(-P)).
+// With s < 2^254 the signed c-bit recoding needs W = ceil(255 / c) windows (c = 17: 15).
+__device__ __forceinline__ Fr scalar_half(const Fr* p, bool& neg) {
+  const Fr s = fe_from_mont(ld_fr(p));
+  const Fr t = fe_neg(s);
+  bool lt = false;  // t < s
+#pragma unroll
+  for (int k = 7; k >= 0; --k) {
+    if (t.v[k] != s.v[k]) {
+      lt = t.v[k] < s.v[k];
+      break;
+    }
+  }
+  neg = lt;
+  return lt ? t : s;
+}
+
+// LDS histograms cover at most kLdsBuckets buckets (128 KiB); larger bucket sets (c = 17)
+// are processed in bucket windows, each a fresh pass over the workgroup's scalars.
+constexpr uint32_t kLdsBuckets = 32768;
+
+// Pass 1: LDS histogram of this workgroup's digits, written whole to
+// blockhist[slot][blk][b] (no global atomics).
 __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cfg,
-                                                       uint32_t* __restrict__ counts) {
+                                                       uint32_t* __restrict__ blockhist) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
   const uint32_t slot = blockIdx.y, B = cfg.B;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
-  __syncthreads();
   uint32_t i0, i1;
   slot_range(batch.len[slot], i0, i1);
   const Fr* sc = batch.scalars[slot];
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const Fr s = fe_from_mont(ld_fr(&sc[i]));
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg.c, carry);
-      if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+  uint32_t* out = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * B;
+  for (uint32_t b0 = 0; b0 < B; b0 += kLdsBuckets) {
+    const uint32_t nb = min(kLdsBuckets, B - b0);
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+      bool neg;
+      const Fr s = scalar_half(&sc[i], neg);
+      uint32_t carry = 0;
+      for (uint32_t w = 0; w < cfg.W; ++w) {
+        const int d = digit_at(s, w, cfg.c, carry);
+        const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;  // wraps for d == 0
+        if (d != 0 && b < nb) atomicAdd(&hist[b], 1u);
+      }
     }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) out[b0 + b] = hist[b];
+    __syncthreads();
   }
-  __syncthreads();
-  uint32_t* cnt = counts + (size_t)slot * B;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x)
-    if (hist[b]) atomicAdd(&cnt[b], hist[b]);
 }
 
-// single workgroup per slot: offsets = exclusive scan(counts) (also the scatter cursors),
+// Per bucket, over the histogram workgroups: blockhist becomes the exclusive running count
+// (each workgroup's first position inside the bucket) and counts[b] the bucket total.
+__global__ void k_block_scan(uint32_t* __restrict__ blockhist, uint32_t nblk, uint32_t B,
+                             uint32_t* __restrict__ counts) {
+  const uint32_t slot = blockIdx.y;
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  uint32_t* h = blockhist + (size_t)slot * nblk * B + b;
+  uint32_t run = 0;
+  for (uint32_t k = 0; k < nblk; ++k) {
+    const uint32_t v = h[(size_t)k * B];
+    h[(size_t)k * B] = run;
+    run += v;
+  }
+  counts[(size_t)slot * B + b] = run;
+}
+
+// single workgroup per slot: offsets = exclusive scan(counts),
 // task_off = exclusive scan(ceil(count / CH)) (where each bucket's partial sums go), and the
 // EXECUTION order of the tasks: all full tasks (CH entries) first in bucket order, then the
 // partial tails grouped by length, longest first, so that a wavefront's lanes run tasks of
@@ -96,7 +143,6 @@ __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restric
                                                        uint32_t B, uint32_t chunk,
                                                        uint32_t* __restrict__ offsets,
                                                        uint32_t* __restrict__ task_off,
-                                                       uint32_t* __restrict__ cursor,
                                                        uint32_t* __restrict__ full_off,
                                                        uint32_t* __restrict__ len_cur) {
   __shared__ uint32_t s_cnt[1024], s_tsk[1024], s_full[1024], s_len[kChunkMax];
@@ -104,7 +150,6 @@ __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restric
   counts += (size_t)slot * B;
   offsets += (size_t)slot * (B + 1);
   task_off += (size_t)slot * (B + 1);
-  cursor += (size_t)slot * B;
   full_off += (size_t)slot * B;
   len_cur += (size_t)slot * kChunkMax;
   const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -136,7 +181,6 @@ __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restric
   uint32_t c_run = s_cnt[tid] - c_sum, t_run = s_tsk[tid] - t_sum, f_run = s_full[tid] - f_sum;
   for (uint32_t b = b0; b < b0 + per && b < B; ++b) {
     offsets[b] = c_run;
-    cursor[b] = c_run;
     task_off[b] = t_run;
     full_off[b] = f_run;
     c_run += counts[b];
@@ -156,44 +200,40 @@ __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restric
   }
 }
 
-// Pass 2: same histogram again, reserve this workgroup's range of every bucket with one
-// global atomic per bucket, then place each digit with an LDS atomic on the reservation.
+// Pass 2: this workgroup's positions start at offsets[b] + blockhist[slot][blk][b]; each
+// digit takes the next one with an LDS atomic (bucket windows as in k_hist).
 __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg cfg,
                                                           uint64_t n_srs,
-                                                          uint32_t* __restrict__ cursor,
+                                                          const uint32_t* __restrict__ offsets,
+                                                          const uint32_t* __restrict__ blockhist,
                                                           uint32_t* __restrict__ sorted,
                                                           uint64_t sorted_stride) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
   const uint32_t slot = blockIdx.y, B = cfg.B;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
-  __syncthreads();
+  const uint32_t* off = offsets + (size_t)slot * (B + 1);
+  const uint32_t* bh = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * B;
   uint32_t i0, i1;
   slot_range(batch.len[slot], i0, i1);
   const Fr* sc = batch.scalars[slot];
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const Fr s = fe_from_mont(ld_fr(&sc[i]));
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg.c, carry);
-      if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
-    }
-  }
-  __syncthreads();
-  uint32_t* cur = cursor + (size_t)slot * B;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x)
-    if (hist[b]) hist[b] = atomicAdd(&cur[b], hist[b]);
-  __syncthreads();
   uint32_t* out = sorted + (size_t)slot * sorted_stride;
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const Fr s = fe_from_mont(ld_fr(&sc[i]));
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg.c, carry);
-      if (d != 0) {
-        const uint32_t pos = atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
-        out[pos] = (uint32_t)(w * n_srs + i) | (d < 0 ? 0x80000000u : 0u);
+  for (uint32_t b0 = 0; b0 < B; b0 += kLdsBuckets) {
+    const uint32_t nb = min(kLdsBuckets, B - b0);
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = off[b0 + b] + bh[b0 + b];
+    __syncthreads();
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+      bool neg;
+      const Fr s = scalar_half(&sc[i], neg);
+      uint32_t carry = 0;
+      for (uint32_t w = 0; w < cfg.W; ++w) {
+        const int d = digit_at(s, w, cfg.c, carry);
+        const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;
+        if (d != 0 && b < nb) {
+          const uint32_t pos = atomicAdd(&hist[b], 1u);
+          out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
+        }
       }
     }
+    __syncthreads();
   }
 }
 
@@ -284,55 +324,80 @@ __global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* 
   st_g1r(&partials[(size_t)slot * task_stride + pidx], g1r_lazy_finish(acc));
 }
 
-__global__ void __launch_bounds__(128) k_bucket_reduce(const uint32_t* __restrict__ task_off,
-                                                       uint32_t B, uint64_t task_stride,
-                                                       const G1xyzz* __restrict__ partials,
-                                                       G1xyzz* __restrict__ buckets) {
-  const uint32_t slot = blockIdx.y;
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+// Bucket reduction sum_b (b+1) S_b, split per workgroup g of 256 buckets (weights
+// w = 256g + v, v in [1, 256]):
+//   sum_v v S_(g,v) = sum_(j<8) 2^j T_j(g) + 2^8 S_(g,256),  T_j(g) = sum of S_(g,v), bit j of v
+//   sum_g 256 g A_g = sum_i 2^(8+i) sum_(g: bit i of g) A_g,  A_g = sum_v S_(g,v).
+// k_bitsum1 (one workgroup of 256 lanes per g, two per CU): the bucket sums S from the
+// accumulation partials, then T_0..T_7 (the 128 buckets with bit j set are enumerated
+// directly: 4 additions per lane, no divergent skips), and A_g = T_0 + (even buckets), each
+// finished by a 32-way LDS tree. out[slot][g][0..7] = T_j(g), [8] = A_g, [9] = S_(g,256).
+constexpr uint32_t kBitsumOut = 10;
+
+__global__ void __launch_bounds__(256) k_bitsum1(const uint32_t* __restrict__ task_off, uint32_t B,
+                                                 uint64_t task_stride,
+                                                 const G1xyzz* __restrict__ partials,
+                                                 G1xyzz* __restrict__ out) {
+  __shared__ G1xyzz sh[288];  // [0, 256): buckets, then group partials; [256, 288): T_0
+  const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
   task_off += (size_t)slot * (B + 1);
   partials += (size_t)slot * task_stride;
-  G1R acc = g1r_infinity();
-  for (uint32_t t = task_off[b]; t < task_off[b + 1]; ++t) acc = g1r_add(acc, ld_g1r(&partials[t]));
-  st_g1r(&buckets[(size_t)slot * B + b], acc);
-}
-
-// Workgroup g owns buckets [256g, 256g+256). Thread (j, s) sums the 16 buckets
-// 256g + 16s + u whose weight (b+1) has bit j set; then a 16-way LDS tree per j.
-// out[slot][g * nbits + j]
-__global__ void __launch_bounds__(256) k_bitsum1(const G1xyzz* __restrict__ buckets, uint32_t B,
-                                                 uint32_t nbits, G1xyzz* __restrict__ out) {
-  __shared__ G1xyzz sh[256];
-  const uint32_t slot = blockIdx.y;
-  buckets += (size_t)slot * B;
-  out += (size_t)slot * gridDim.x * nbits;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t j = tid >> 4, s = tid & 15;
-  G1R acc = g1r_infinity();
-  if (j < nbits) {
-    for (uint32_t u = 0; u < 16; ++u) {
-      const uint32_t b = blockIdx.x * 256 + s * 16 + u;
-      if (b < B && (((b + 1) >> j) & 1u)) acc = g1r_add(acc, ld_g1r(&buckets[b]));
-    }
+  out += ((size_t)slot * gridDim.x + g) * kBitsumOut;
+  {
+    const uint32_t b = g * 256 + tid;
+    G1R acc = g1r_infinity();
+    if (b < B)
+      for (uint32_t t = task_off[b]; t < task_off[b + 1]; ++t) acc = g1r_add(acc, ld_g1r(&partials[t]));
+    st_g1r(&sh[tid], acc);
   }
+  __syncthreads();
+  const uint32_t j = tid >> 5, s = tid & 31;
+  G1R acc = g1r_infinity();
+#pragma unroll 1
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint32_t k = 4 * s + q;
+    const uint32_t v = ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
+    acc = g1r_add(acc, ld_g1r(&sh[v - 1]));
+  }
+  if (j == 0) {  // group 0 keeps its T_0 partial and goes on with the even buckets: A_g
+    st_g1r(&sh[256 + s], acc);
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) acc = g1r_add(acc, ld_g1r(&sh[2 * (4 * s + q) + 1]));
+  }
+  if (tid == 255) out[9] = sh[255];
+  __syncthreads();
   st_g1r(&sh[tid], acc);
   __syncthreads();
-  for (uint32_t h = 8; h >= 1; h >>= 1) {
-    if (s < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
+  for (uint32_t h = 16; h >= 1; h >>= 1) {
+    if (s < h) {
+      st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
+      if (j == 0) st_g1r(&sh[256 + s], g1r_add(ld_g1r(&sh[256 + s]), ld_g1r(&sh[256 + s + h])));
+    }
     __syncthreads();
   }
-  if (s == 0 && j < nbits) out[blockIdx.x * nbits + j] = sh[tid];
+  if (s == 0) {
+    out[j == 0 ? 8 : j] = sh[tid];
+    if (j == 0) out[0] = sh[256];
+  }
 }
 
-// Workgroup j of slot sums in[slot][g * nbits + j] over g < G.
+// Workgroup j of slot: T_j = sum_g T_j(g) for j < 8; T_8 = sum_g S_(g,256) + sum_(g odd) A_g;
+// T_(8+i) = sum_(g: bit i of g) A_g.
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, G1xyzz* __restrict__ out) {
   __shared__ G1xyzz sh[256];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
-  in += (size_t)slot * G * nbits;
+  in += (size_t)slot * G * kBitsumOut;
   G1R acc = g1r_infinity();
-  for (uint32_t g = tid; g < G; g += 256) acc = g1r_add(acc, ld_g1r(&in[g * nbits + j]));
+  for (uint32_t g = tid; g < G; g += 256) {
+    const G1xyzz* e = &in[(size_t)g * kBitsumOut];
+    if (j < 8) {
+      acc = g1r_add(acc, ld_g1r(&e[j]));
+    } else {
+      if ((g >> (j - 8)) & 1u) acc = g1r_add(acc, ld_g1r(&e[8]));
+      if (j == 8) acc = g1r_add(acc, ld_g1r(&e[9]));
+    }
+  }
   st_g1r(&sh[tid], acc);
   __syncthreads();
   for (uint32_t h = 128; h >= 1; h >>= 1) {
@@ -383,19 +448,18 @@ int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
   if ((st = w.counts.alloc(slots * B * 4))) return st;
   if ((st = w.offsets.alloc(slots * (B + 1) * 4))) return st;
   if ((st = w.task_off.alloc(slots * (B + 1) * 4))) return st;
-  if ((st = w.cursor.alloc(slots * B * 4))) return st;
+  if ((st = w.blockhist.alloc(slots * kHistBlocksMax * B * 4))) return st;
   if ((st = w.full_off.alloc(slots * B * 4))) return st;
   if ((st = w.len_cur.alloc(slots * kChunkMax * 4))) return st;
   if ((st = w.sorted.alloc(slots * (entries + 1) * 4))) return st;
   if ((st = w.tasks.alloc(slots * max_tasks * sizeof(uint2)))) return st;
   if ((st = w.partials.alloc(slots * max_tasks * sizeof(G1xyzz)))) return st;
-  if ((st = w.buckets.alloc(slots * B * sizeof(G1xyzz)))) return st;
-  if ((st = w.bits1.alloc(slots * G * s->c * sizeof(G1xyzz)))) return st;
+  if ((st = w.bits1.alloc(slots * G * kBitsumOut * sizeof(G1xyzz)))) return st;
   if ((st = w.bits2.alloc(slots * s->c * sizeof(G1xyzz)))) return st;
   if ((st = w.flag.alloc(slots * 4 + 16))) return st;
   if (!w.ev0) PLK_HIP_TRY(hipEventCreate(&w.ev0));
   if (!w.ev1) PLK_HIP_TRY(hipEventCreate(&w.ev1));
-  const int lds = (int)(B * 4);
+  const int lds = (int)(std::min<uint32_t>((uint32_t)B, kLdsBuckets) * 4);
   PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scatter),
@@ -443,27 +507,32 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
   // 256 workgroups per slot: fewer give longer per-bucket write runs in k_scatter but lose
   // more parallelism than they gain (measured 2.77 / 2.79 / 3.02 / 4.52 ms per proof at
   // 256 / 128 / 64 / 32, tools/gpu_hist_sweep.sh)
-  const uint32_t hist_blocks = std::max<uint32_t>(1, std::min<uint32_t>(256, cdiv(max_len, 512)));
+  const uint32_t hist_blocks =
+      std::max<uint32_t>(1, std::min<uint32_t>(kHistBlocksMax, cdiv(max_len, 512)));
 
   PLK_HIP_TRY(hipMemsetAsync(w.flag.ptr, 0, slots * 4, stream));
   if (max_tail) {
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
                        batch, w.flag.as<uint32_t>());
   }
-  PLK_HIP_TRY(hipMemsetAsync(w.counts.ptr, 0, (size_t)slots * B * 4, stream));
-  const size_t lds = (size_t)B * 4;
+  const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
   if (max_len) {
     hipLaunchKernelGGL(k_hist, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream, batch,
-                       cfg, w.counts.as<uint32_t>());
+                       cfg, w.blockhist.as<uint32_t>());
+  } else {
+    PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * B * 4, stream));
   }
+  hipLaunchKernelGGL(k_block_scan, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
+                     w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>());
   hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
                      w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
-                     w.task_off.as<uint32_t>(), w.cursor.as<uint32_t>(),
-                     w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>());
+                     w.task_off.as<uint32_t>(), w.full_off.as<uint32_t>(),
+                     w.len_cur.as<uint32_t>());
   if (max_len) {
     hipLaunchKernelGGL(k_scatter, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream,
-                       batch, cfg, (uint64_t)s->n, w.cursor.as<uint32_t>(),
-                       w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride);
+                       batch, cfg, (uint64_t)s->n, w.offsets.as<uint32_t>(),
+                       w.blockhist.as<uint32_t>(), w.sorted.as<uint32_t>(),
+                       (uint64_t)w.sorted_stride);
   }
   hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
                      w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),
@@ -484,11 +553,8 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
                        s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
   }
   PLK_HIP_TRY(hipEventRecord(w.ev1, stream));
-  hipLaunchKernelGGL(k_bucket_reduce, dim3(cdiv(B, 128), slots), dim3(128), 0, stream,
-                     w.task_off.as<uint32_t>(), B, (uint64_t)w.task_stride,
-                     w.partials.as<G1xyzz>(), w.buckets.as<G1xyzz>());
-  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, w.buckets.as<G1xyzz>(), B,
-                     nbits, w.bits1.as<G1xyzz>());
+  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, w.task_off.as<uint32_t>(), B,
+                     (uint64_t)w.task_stride, w.partials.as<G1xyzz>(), w.bits1.as<G1xyzz>());
   hipLaunchKernelGGL(k_bitsum2, dim3(nbits, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
                      G, nbits, w.bits2.as<G1xyzz>());
   PLK_HIP_TRY(hipGetLastError());

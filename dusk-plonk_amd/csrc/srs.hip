@@ -92,9 +92,13 @@ __global__ void __launch_bounds__(256) k_table_to_rx(G1Affine* __restrict__ tab,
 
 }  // namespace
 
-// Window size for an SRS of n points (bucket count 2^(c-1); table W*n).
+// Window size for an SRS of n points (bucket count 2^(c-1); table W*n, W = ceil(255/c)).
 static uint32_t choose_c(size_t n) {
-  if (n >= (1u << 18)) return 16;
+  // c = 17: 15 windows of the half-range scalars (msm.hip scalar_half) against 16 at c = 16
+#ifndef PLK_C_LARGE
+#define PLK_C_LARGE 16  // 17 (15 windows) measured slower end to end: its 2x buckets cost more in the sort and reduction kernels than the 6% fewer entries save
+#endif
+  if (n >= (1u << 18)) return PLK_C_LARGE;
   if (n >= (1u << 14)) return 13;
   if (n >= (1u << 10)) return 10;
   return 8;
@@ -102,7 +106,7 @@ static uint32_t choose_c(size_t n) {
 
 int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   s->c = choose_c(s->n);
-  s->windows = (256 + s->c - 1) / s->c;
+  s->windows = (255 + s->c - 1) / s->c;  // scalars recoded from [0, (r-1)/2] (< 2^254)
   const size_t n = s->n;
   int st;
   if ((st = s->table.alloc((size_t)s->windows * n * sizeof(G1Affine)))) return st;

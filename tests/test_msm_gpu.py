@@ -50,12 +50,13 @@ def test_commit_strips_trailing_zeros_and_errs_past_srs(plk, srs_small, golden):
     assert srs_small.commit(plk.Coefficients(np.zeros((0, 4), np.uint64))).is_identity
 
 
-@pytest.mark.parametrize("logn", [7, 10, 12, 14, 16])
+@pytest.mark.parametrize("logn", [7, 10, 12, 14, 16, 18])
 def test_msm_vs_oracle(plk, gpu_ctx, oracle, logn):
     n = 1 << logn
     tau = random_fr(1, seed=logn)[0]
     pp = plk.PlonkParams.setup(logn, tau, gpu_ctx, n_points=n + 8)
     pts = pp.points()
+    # logn = 18: the c = 17 / 15-window configuration of n >= 2^18 (srs.hip choose_c)
     if logn <= 12:  # the SRS itself against the oracle's setup
         assert np.array_equal(pts, oracle.srs(tau, n + 8))
     sc = random_fr(n, seed=1000 + logn)
@@ -67,6 +68,10 @@ def test_msm_vs_oracle(plk, gpu_ctx, oracle, logn):
         "tiny": P.fr_vec_to_np([i % 5 for i in range(n)]),
         "sparse": np.where((np.arange(n) % 17 == 0)[:, None], sc, 0).astype(np.uint64),
         "minus_one": np.tile(fr_int(P.R_MOD - 1), (n, 1)),
+        # around the half-range recoding boundary (msm.hip scalar_half: s > (r-1)/2 -> r - s)
+        "half_boundary": P.fr_vec_to_np([
+            [(P.R_MOD - 1) // 2, (P.R_MOD + 1) // 2, (P.R_MOD - 1) // 2 - 1, (P.R_MOD + 3) // 2,
+             1 << 253, P.R_MOD - (1 << 253), (1 << 254) - 1, P.R_MOD - 2][i % 8] for i in range(n)]),
     }
     for name, s in cases.items():
         assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), name
