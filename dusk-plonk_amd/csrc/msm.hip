@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
 // Task t of bucket b covers sorted[offsets[b] + t*CH, ...+CH) and writes its partial sum to
 // partials[task_off[b] + t]; its execution slot is full_off[b] + t for a full task, or the
 // next slot of its length class for the tail. tasks[slot] = {first entry, partial index |
-// (length - 1) << 26}.
+// (length - 1) << kTaskShift}.
 __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
                              const uint32_t* __restrict__ task_off,
                              const uint32_t* __restrict__ full_off, uint32_t* __restrict__ len_cur,
@@ -256,10 +256,10 @@ __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
   const uint32_t t0 = task_off[b], nfull = cnt / chunk;
   uint32_t x = full_off[(size_t)slot * B + b];
   for (uint32_t t = 0; t < nfull; ++t, ++x)
-    tasks[x] = make_uint2(start + t * chunk, (t0 + t) | ((chunk - 1) << 26));
+    tasks[x] = make_uint2(start + t * chunk, (t0 + t) | ((chunk - 1) << kTaskShift));
   if (const uint32_t tail = cnt - nfull * chunk) {
     const uint32_t e = atomicAdd(&len_cur[(size_t)slot * kChunkMax + tail], 1u);
-    tasks[e] = make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << 26));
+    tasks[e] = make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << kTaskShift));
   }
 }
 
@@ -279,8 +279,8 @@ __global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* 
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= task_off[(size_t)slot * (B + 1) + B]) return;
   const uint2 tk = tasks[(size_t)slot * task_stride + t];
-  const uint2 task = make_uint2(tk.x, (tk.y >> 26) + 1);  // first entry, length (>= 1)
-  const uint32_t pidx = tk.y & ((1u << 26) - 1);
+  const uint2 task = make_uint2(tk.x, (tk.y >> kTaskShift) + 1);  // first entry, length (>= 1)
+  const uint32_t pidx = tk.y & ((1u << kTaskShift) - 1);
   sorted += (size_t)slot * sorted_stride;
   // software-pipelined: the next entry's index and point are loaded before the current
   // mixed add, so the two dependent loads overlap the ~5k-instruction madd (+8%,
@@ -443,7 +443,7 @@ int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
   const size_t entries = (size_t)s->windows * len;
   const size_t max_tasks = entries / kChunkMin + B + 1;
   const size_t G = (B + 255) / 256;
-  if (max_tasks >= ((size_t)1 << 26)) return PLK_E_ARG;  // task records hold 26-bit partial indices
+  if (max_tasks >= ((size_t)1 << kTaskShift)) return PLK_E_ARG;  // task records: partial index bits
   int st;
   if ((st = w.counts.alloc(slots * B * 4))) return st;
   if ((st = w.offsets.alloc(slots * (B + 1) * 4))) return st;

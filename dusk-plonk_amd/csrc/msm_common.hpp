@@ -4,8 +4,14 @@
 
 namespace plk {
 
+#ifndef PLK_CHUNK_MAX
+#define PLK_CHUNK_MAX 64
+#endif
 constexpr uint32_t kChunkMin = 16;  // points per accumulation task (bounds)
-constexpr uint32_t kChunkMax = 64;
+constexpr uint32_t kChunkMax = PLK_CHUNK_MAX;
+// task record .y = partial index | (length - 1) << kTaskShift
+constexpr uint32_t kTaskShift = 32 - (kChunkMax <= 64 ? 6 : 7);
+static_assert(kChunkMax <= 128, "task length field");
 constexpr uint32_t kBatchAff = 32;  // points per batch-inversion chunk
 constexpr uint32_t kMaxSlots = 16;  // independent MSMs per batch
 
