@@ -37,6 +37,9 @@ namespace plk {
 
 namespace {
 
+#ifndef PLK_XCD_RANK
+#define PLK_XCD_RANK 0
+#endif
 constexpr uint32_t kHistThreads = 1024;
 constexpr uint32_t kHistBlocksMax = 256;  // histogram / scatter workgroups per slot
 
@@ -60,9 +63,22 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, uint32_t c, uin
   return d;
 }
 
+// Rank of this histogram / scatter workgroup among the slot's gridDim.x: workgroups are
+// dispatched round-robin over the 8 XCDs (blockIdx.x % 8), so the ranks of one XCD are made
+// consecutive — their digits land next to each other inside every bucket's segment of the
+// sorted array, and k_scatter's 4-byte writes then share cache lines within one XCD's L2.
+__device__ __forceinline__ uint32_t wg_rank() {
+#if PLK_XCD_RANK
+  const uint32_t n = gridDim.x, x = blockIdx.x;
+  return (n & 7u) ? x : (x & 7u) * (n >> 3) + (x >> 3);
+#else
+  return blockIdx.x;
+#endif
+}
+
 __device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t& i1) {
   const uint32_t per = (len + gridDim.x - 1) / gridDim.x;
-  i0 = blockIdx.x * per;
+  i0 = wg_rank() * per;
   i1 = min(len, i0 + per);
 }
 
@@ -96,7 +112,7 @@ __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cf
   uint32_t i0, i1;
   slot_range(batch.len[slot], i0, i1);
   const Fr* sc = batch.scalars[slot];
-  uint32_t* out = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * B;
+  uint32_t* out = blockhist + ((size_t)slot * gridDim.x + wg_rank()) * B;
   for (uint32_t b0 = 0; b0 < B; b0 += kLdsBuckets) {
     const uint32_t nb = min(kLdsBuckets, B - b0);
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
@@ -211,7 +227,7 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
   const uint32_t slot = blockIdx.y, B = cfg.B;
   const uint32_t* off = offsets + (size_t)slot * (B + 1);
-  const uint32_t* bh = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * B;
+  const uint32_t* bh = blockhist + ((size_t)slot * gridDim.x + wg_rank()) * B;
   uint32_t i0, i1;
   slot_range(batch.len[slot], i0, i1);
   const Fr* sc = batch.scalars[slot];
@@ -324,21 +340,29 @@ __global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* 
   st_g1r(&partials[(size_t)slot * task_stride + pidx], g1r_lazy_finish(acc));
 }
 
-// Bucket reduction sum_b (b+1) S_b, split per workgroup g of 256 buckets (weights
-// w = 256g + v, v in [1, 256]):
-//   sum_v v S_(g,v) = sum_(j<8) 2^j T_j(g) + 2^8 S_(g,256),  T_j(g) = sum of S_(g,v), bit j of v
-//   sum_g 256 g A_g = sum_i 2^(8+i) sum_(g: bit i of g) A_g,  A_g = sum_v S_(g,v).
-// k_bitsum1 (one workgroup of 256 lanes per g, two per CU): the bucket sums S from the
-// accumulation partials, then T_0..T_7 (the 128 buckets with bit j set are enumerated
-// directly: 4 additions per lane, no divergent skips), and A_g = T_0 + (even buckets), each
-// finished by a 32-way LDS tree. out[slot][g][0..7] = T_j(g), [8] = A_g, [9] = S_(g,256).
-constexpr uint32_t kBitsumOut = 10;
+// Bucket reduction sum_b (b+1) S_b, split per workgroup g of 256 buckets b = 256g + u,
+// u = 16a + c (a, c < 16):
+//   sum_u (256g + u + 1) S_(g,u) = sum_(j<8) 2^j T_j(g) + (256g + 1) A_g,
+//   T_j(g) = sum of S_(g,u) over u with bit j set,  A_g = sum_u S_(g,u).
+// With row sums Row_a = sum_c S_(g,16a+c) and column sums Col_c = sum_a S_(g,16a+c), T_j for
+// j < 4 is a sum of the 8 columns with bit j of c set and T_(4+i) a sum of the 8 rows with
+// bit i of a set; A_g is the sum of the rows: 480 + 71 additions per 256 buckets instead of
+// the 1 144 of bit sums taken over the buckets themselves.
+// k_bitsum1 (one workgroup of 256 lanes per g): the bucket sums S from the accumulation
+// partials, the 32 row / column sums (8 lanes each: one addition, then a 3-level LDS tree),
+// then the 9 outputs from them (wave 0). out[slot][g][0..7] = T_j(g), [8] = A_g.
+constexpr uint32_t kBitsumOut = 9;
+
+// k-th of the 8 indices in [0, 16) with bit j set
+__device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
+  return ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
+}
 
 __global__ void __launch_bounds__(256) k_bitsum1(const uint32_t* __restrict__ task_off, uint32_t B,
                                                  uint64_t task_stride,
                                                  const G1xyzz* __restrict__ partials,
                                                  G1xyzz* __restrict__ out) {
-  __shared__ G1xyzz sh[288];  // [0, 256): buckets, then group partials; [256, 288): T_0
+  __shared__ G1xyzz sh[256 + 32];  // [0, 256): buckets, then tree partials; [256, 288): rows, columns
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
   task_off += (size_t)slot * (B + 1);
   partials += (size_t)slot * task_stride;
@@ -351,37 +375,52 @@ __global__ void __launch_bounds__(256) k_bitsum1(const uint32_t* __restrict__ ta
     st_g1r(&sh[tid], acc);
   }
   __syncthreads();
-  const uint32_t j = tid >> 5, s = tid & 31;
-  G1R acc = g1r_infinity();
-#pragma unroll 1
-  for (uint32_t q = 0; q < 4; ++q) {
-    const uint32_t k = 4 * s + q;
-    const uint32_t v = ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
-    acc = g1r_add(acc, ld_g1r(&sh[v - 1]));
-  }
-  if (j == 0) {  // group 0 keeps its T_0 partial and goes on with the even buckets: A_g
-    st_g1r(&sh[256 + s], acc);
-#pragma unroll 1
-    for (uint32_t q = 0; q < 4; ++q) acc = g1r_add(acc, ld_g1r(&sh[2 * (4 * s + q) + 1]));
-  }
-  if (tid == 255) out[9] = sh[255];
-  __syncthreads();
-  st_g1r(&sh[tid], acc);
-  __syncthreads();
-  for (uint32_t h = 16; h >= 1; h >>= 1) {
-    if (s < h) {
-      st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
-      if (j == 0) st_g1r(&sh[256 + s], g1r_add(ld_g1r(&sh[256 + s]), ld_g1r(&sh[256 + s + h])));
+  {  // sum q < 16: row a = q; q >= 16: column c = q - 16. Lane e of its 8 adds members 2e, 2e + 1.
+    const uint32_t q = tid >> 3, e = tid & 7;
+    const uint32_t m0 = q < 16 ? 16 * q + 2 * e : (q - 16) + 32 * e;
+    const uint32_t m1 = q < 16 ? m0 + 1 : m0 + 16;
+    const G1R acc = g1r_add(ld_g1r(&sh[m0]), ld_g1r(&sh[m1]));
+    __syncthreads();
+    st_g1r(&sh[tid], acc);
+    __syncthreads();
+    for (uint32_t h = 4; h >= 1; h >>= 1) {
+      if (e < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
+      __syncthreads();
     }
+    if (e == 0) sh[256 + q] = sh[tid];
     __syncthreads();
   }
-  if (s == 0) {
-    out[j == 0 ? 8 : j] = sh[tid];
-    if (j == 0) out[0] = sh[256];
+  // wave 0: lanes 0..31 = T_0..T_7, 4 lanes each (2 terms per lane); lanes 32..39 = A_g, 8 lanes
+  // (rows 2e, 2e + 1); then trees
+  if (tid < 40) {
+    const uint32_t s = tid < 32 ? tid >> 2 : 8, e = tid < 32 ? tid & 3 : tid - 32;
+    const uint32_t w = tid < 32 ? 4 : 8;
+    uint32_t i0, i1;
+    if (s < 4) {  // columns c with bit s
+      i0 = 256 + 16 + with_bit(2 * e, s);
+      i1 = 256 + 16 + with_bit(2 * e + 1, s);
+    } else if (s < 8) {  // rows a with bit s - 4
+      i0 = 256 + with_bit(2 * e, s - 4);
+      i1 = 256 + with_bit(2 * e + 1, s - 4);
+    } else {
+      i0 = 256 + 2 * e;
+      i1 = i0 + 1;
+    }
+    st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[i0]), ld_g1r(&sh[i1])));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (uint32_t h = 4; h >= 1; h >>= 1) {
+      if (e < h && h < w) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    if (e == 0) out[s] = sh[tid];
   }
 }
 
-// Workgroup j of slot: T_j = sum_g T_j(g) for j < 8; T_8 = sum_g S_(g,256) + sum_(g odd) A_g;
+// Workgroup j of slot: T_j = sum_g T_j(g) for 0 < j < 8; T_0 = sum_g (T_0(g) + A_g);
 // T_(8+i) = sum_(g: bit i of g) A_g.
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, G1xyzz* __restrict__ out) {
@@ -393,9 +432,9 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
     const G1xyzz* e = &in[(size_t)g * kBitsumOut];
     if (j < 8) {
       acc = g1r_add(acc, ld_g1r(&e[j]));
-    } else {
-      if ((g >> (j - 8)) & 1u) acc = g1r_add(acc, ld_g1r(&e[8]));
-      if (j == 8) acc = g1r_add(acc, ld_g1r(&e[9]));
+      if (j == 0) acc = g1r_add(acc, ld_g1r(&e[8]));
+    } else if ((g >> (j - 8)) & 1u) {
+      acc = g1r_add(acc, ld_g1r(&e[8]));
     }
   }
   st_g1r(&sh[tid], acc);
@@ -455,7 +494,7 @@ int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
   if ((st = w.tasks.alloc(slots * max_tasks * sizeof(uint2)))) return st;
   if ((st = w.partials.alloc(slots * max_tasks * sizeof(G1xyzz)))) return st;
   if ((st = w.bits1.alloc(slots * G * kBitsumOut * sizeof(G1xyzz)))) return st;
-  if ((st = w.bits2.alloc(slots * s->c * sizeof(G1xyzz)))) return st;
+  if ((st = w.bits2.alloc(slots * 32 * sizeof(G1xyzz)))) return st;  // nbits <= 32
   if ((st = w.flag.alloc(slots * 4 + 16))) return st;
   if (!w.ev0) PLK_HIP_TRY(hipEventCreate(&w.ev0));
   if (!w.ev1) PLK_HIP_TRY(hipEventCreate(&w.ev1));
@@ -497,8 +536,8 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
   MsmWorkspace& w = *s->ws;
   const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1)};
   const uint32_t B = cfg.B;
-  const uint32_t nbits = s->c;  // weights b+1 in [1, 2^(c-1)] need c bits
-  const uint32_t G = cdiv(B, 256);
+  const uint32_t G = cdiv(B, 256);  // a power of two
+  const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
   const uint32_t slots = (uint32_t)count;
   // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads
   const uint32_t chunk = (uint32_t)std::min<size_t>(
