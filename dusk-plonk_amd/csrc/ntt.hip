@@ -67,7 +67,14 @@ __device__ __forceinline__ RFr ld_rfr(const Fr* p) { return rx_unpack(ld_fr(p));
 // POST: 0 none, 1 multiply by post_scalar, 2 multiply output e by post[e].
 // Data buffers are R-domain (canonical in and out); tw / pre / post / post_scalar are
 // R'-domain (ffr.hpp), so every product data x table stays in the R domain.
-template <int PRE, int POST>
+//
+// PRUNE (first pass of a multi-pass plan, input nonzero only in rows j <= R/8 of the pass):
+// the first three DIF stages of a zero-padded column have the closed form
+//   y[t R/8 + j] = w_R^(j b) (x_j + x_(j+R/8) w_8^b),  b = bitrev3(t),
+// with x_(j+R/8) = 0 except for j = 0 — the 8n coset transforms of the prover's
+// (n + small)-coefficient polynomials. They are computed directly from the loaded rows
+// (7 multiplies per row instead of three stages of butterflies over 8x the rows).
+template <int PRE, int POST, int PRUNE>
 __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                   const Fr* __restrict__ tw,
                                                   const Fr* __restrict__ ptw,
@@ -78,8 +85,10 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const uint32_t R = 1u << lr, T = 1u << lt, p = 1u << lp;
   const uint32_t E = R << lt, H = R >> 1;
+  // kL planes of the TS inner twiddles w_R^x (x < R/2; x < R when pruning)
+  const uint32_t TS = PRUNE ? R : H;
   uint32_t* data = smem32;          // kL planes of E
-  uint32_t* twl = smem32 + kL * E;  // kL planes of R/2 inner twiddles w_R^x
+  uint32_t* twl = smem32 + kL * E;
 
   const size_t voff = (size_t)blockIdx.y * n_stride;
   in += voff;
@@ -89,9 +98,37 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   const uint32_t nr_log = log_n - lr;  // log2(N/R)
   const uint32_t i0 = blockIdx.x << lt;
 
-  for (uint32_t x = tid; x < H; x += bd) lds_st(twl, H, x, ld_rfr(&tw[(size_t)x << nr_log]));
+  for (uint32_t x = tid; x < TS; x += bd) lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
 
-  for (uint32_t e = tid; e < E; e += bd) {
+  if (PRUNE) {
+    __syncthreads();
+    // item = (row j < R/8, column t, half hs): blocks 4 hs .. 4 hs + 3 of (j, t)
+    const uint32_t R8 = R >> 3;
+    for (uint32_t it = tid; it < (E >> 2); it += bd) {
+      const uint32_t hs = it & 1, t = (it >> 1) & (T - 1), j = it >> (lt + 1);
+      const uint32_t i = i0 + t;
+      const size_t g = (size_t)i + ((size_t)j << nr_log);
+      RFr x = rx_zero<FrCfg>(), x8 = rx_zero<FrCfg>();
+      if (g < len_in) {
+        x = ld_rfr(&in[g]);
+        if (PRE == 1) x = rx_mul(x, ld_rfr(&pre[g]));
+      }
+      const size_t g8 = (size_t)i + ((size_t)R8 << nr_log);
+      const bool has8 = j == 0 && g8 < len_in;
+      if (has8) {
+        x8 = ld_rfr(&in[g8]);
+        if (PRE == 1) x8 = rx_mul(x8, ld_rfr(&pre[g8]));
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t blk = 4 * hs + q, b = bitrev(blk, 3);
+        RFr v = (j == 0 || b == 0) ? x : rx_mul(x, lds_ld(twl, TS, j * b));
+        if (has8) v = rx_add(v, b == 0 ? x8 : rx_mul(x8, lds_ld(twl, TS, R8 * b)));
+        lds_st(data, E, ((blk * R8 + j) << lt) + t, v);
+      }
+    }
+  }
+  for (uint32_t e = tid; e < (PRUNE ? 0u : E); e += bd) {
     const uint32_t t = e & (T - 1), j = e >> lt;
     const uint32_t i = i0 + t;
     const size_t g = (size_t)i + ((size_t)j << nr_log);
@@ -113,7 +150,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   // per LDS round trip: a thread loads x0..x3 = rows j, j+h, j+2h, j+3h, applies the stage
   // of half 2h (pairs x0/x2, x1/x3) and the stage of half h (pairs y0/y1, y2/y3) in
   // registers, and stores once. Same butterflies and twiddles as stage-by-stage radix 2.
-  int lh = (int)lr - 1;
+  int lh = (int)lr - 1 - (PRUNE ? 3 : 0);
   for (; lh >= 1; lh -= 2) {
     const uint32_t h = 1u << (lh - 1);
     const uint32_t sh1 = lr - 1 - lh, sh2 = lr - lh;  // twiddle index shifts of both stages
@@ -127,13 +164,13 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       const RFr x2 = lds_ld(data, E, i2), x3 = lds_ld(data, E, i3);
       // stage of half 2h: twiddle w^(r s1) for x0/x2 (identity when r = 0), w^((r+h) s1)
       const RFr y0 = rx_add(x0, x2), y1 = rx_add(x1, x3);
-      const RFr y2 = r != 0 ? rx_mul(rx_sub_lazy(x0, x2), lds_ld(twl, H, r << sh1)) : rx_sub(x0, x2);
-      const RFr y3 = rx_mul(rx_sub_lazy(x1, x3), lds_ld(twl, H, (r + h) << sh1));
+      const RFr y2 = r != 0 ? rx_mul(rx_sub_lazy(x0, x2), lds_ld(twl, TS, r << sh1)) : rx_sub(x0, x2);
+      const RFr y3 = rx_mul(rx_sub_lazy(x1, x3), lds_ld(twl, TS, (r + h) << sh1));
       // stage of half h: twiddle w^(r s2) for both pairs
       lds_st(data, E, i0, rx_add(y0, y1));
       lds_st(data, E, i2, rx_add(y2, y3));
       if (r != 0) {
-        const RFr w = lds_ld(twl, H, r << sh2);
+        const RFr w = lds_ld(twl, TS, r << sh2);
         lds_st(data, E, i1, rx_mul(rx_sub_lazy(y0, y1), w));
         lds_st(data, E, i3, rx_mul(rx_sub_lazy(y2, y3), w));
       } else {
@@ -342,24 +379,30 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
     if (bd < 64) bd = 64;
     if (bd > 256) bd = 256;
     const uint32_t blocks = (uint32_t)(n >> (ps.lr + ps.lt));
-    const size_t lds = ((size_t)E + (1u << ps.lr) / 2) * kL * sizeof(uint32_t);
     const int pre = (first && dir > 0 && coset) ? 1 : 0;
     const int post = (last && dir < 0) ? (coset ? 2 : 1) : 0;
     const uint64_t lin = first ? len_in : n;
+    // zero-padded input (rows j <= R/8 of the first pass only): closed-form first stages
+    const bool prune = first && !last && ps.lr >= 4 &&
+                       len_in <= ((n >> ps.lr) << (ps.lr - 3)) + (n >> ps.lr);
+    const size_t lds = ((size_t)E + ((1u << ps.lr) >> (prune ? 0 : 1))) * kL * sizeof(uint32_t);
     dim3 grid(blocks, count);
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
-#define PLK_LAUNCH(PRE, POST)                                                                 \
-  hipLaunchKernelGGL((k_ntt_pass<PRE, POST>), grid, dim3(bd), lds, stream, src, dst, tw, ptw, \
+#define PLK_LAUNCH(PRE, POST, PRUNE)                                                    \
+  hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE>), grid, dim3(bd), lds, stream, src, dst, tw, ptw, \
                      pre_table ? pre_table : d->coset_pow.as<Fr>(), d->icoset_scale.as<Fr>(), \
                      n_inv_rx, d->log_n,                                                      \
                      ps.lp, ps.lr, ps.lt, lin, (uint64_t)n)
-    if (pre == 0 && post == 0) PLK_LAUNCH(0, 0);
-    else if (pre == 1 && post == 0) PLK_LAUNCH(1, 0);
-    else if (pre == 0 && post == 1) PLK_LAUNCH(0, 1);
-    else if (pre == 0 && post == 2) PLK_LAUNCH(0, 2);
-    else if (pre == 1 && post == 1) PLK_LAUNCH(1, 1);
-    else PLK_LAUNCH(1, 2);
+    if (prune) {
+      if (pre == 1) PLK_LAUNCH(1, 0, 1);
+      else PLK_LAUNCH(0, 0, 1);
+    } else if (pre == 0 && post == 0) PLK_LAUNCH(0, 0, 0);
+    else if (pre == 1 && post == 0) PLK_LAUNCH(1, 0, 0);
+    else if (pre == 0 && post == 1) PLK_LAUNCH(0, 1, 0);
+    else if (pre == 0 && post == 2) PLK_LAUNCH(0, 2, 0);
+    else if (pre == 1 && post == 1) PLK_LAUNCH(1, 1, 0);
+    else PLK_LAUNCH(1, 2, 0);
 #undef PLK_LAUNCH
     PLK_HIP_TRY(hipGetLastError());
     src = dst;

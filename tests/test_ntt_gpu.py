@@ -146,3 +146,21 @@ def test_device_entry_points(plk, gpu_ctx, oracle):
     f.ntt_dev(out.data_ptr(), out.data_ptr(), n, -1, True, stream, scratch.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint64), x)
+
+
+@pytest.mark.parametrize("k", [6, 12, 16, 20])
+def test_zero_padded_first_pass(plk, gpu_ctx, oracle, k):
+    """Inputs of at most n/8 + n/R coefficients take the closed-form first stages of the
+    first pass (ntt.hip PRUNE): lengths around both edges of that range, vs the C oracle."""
+    n = 1 << k
+    f = plk.Fft(k, gpu_ctx)
+    x = random_fr(n, seed=300 + k)
+    lens = {0, 1, 2, n // 8 - 1, n // 8, n // 8 + 1, n // 8 + 3, n // 8 + n // 64,
+            n // 8 + n // 64 + 1, n // 8 + n // 128, n // 8 + n // 256, n // 8 + n // 256 + 1}
+    if k == 20:
+        lens = {n // 8, n // 8 + 3, n // 8 + n // 128, n // 8 + n // 128 + 1}
+    for m in sorted(v for v in lens if 0 <= v <= n):
+        xm = x[:m]
+        assert np.array_equal(f.dft(plk.Coefficients(xm)).values, oracle.dft(xm, k)), (k, m)
+        assert np.array_equal(f.coset_dft(plk.Coefficients(xm)).values,
+                              oracle.coset_dft(xm, k)), (k, m)
