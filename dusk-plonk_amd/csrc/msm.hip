@@ -340,6 +340,36 @@ __global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* 
   st_g1r(&partials[(size_t)slot * task_stride + pidx], g1r_lazy_finish(acc));
 }
 
+// Bucket sums S_b = sum of bucket b's accumulation partials (task_off[b] .. task_off[b+1]):
+// 2^lp lanes per bucket, each adding every 2^lp-th partial, then an LDS tree over the lanes
+// (2^lp is sized on the host to the partials per bucket, so the sequential chain stays ~4
+// additions at every MSM size).
+__global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__ task_off,
+                                                    uint32_t B, uint32_t lp, uint64_t task_stride,
+                                                    const G1xyzz* __restrict__ partials,
+                                                    G1xyzz* __restrict__ bsum) {
+  __shared__ G1xyzz sh[256];
+  const uint32_t slot = blockIdx.y, tid = threadIdx.x;
+  const uint32_t P = 1u << lp, s = tid & (P - 1);
+  const uint32_t b = (blockIdx.x * 256 + tid) >> lp;
+  task_off += (size_t)slot * (B + 1);
+  partials += (size_t)slot * task_stride;
+  G1R acc = g1r_infinity();
+  if (b < B)
+    for (uint32_t t = task_off[b] + s; t < task_off[b + 1]; t += P) acc = g1r_add(acc, ld_g1r(&partials[t]));
+  if (P > 1) {
+    st_g1r(&sh[tid], acc);
+    __syncthreads();
+    for (uint32_t h = P >> 1; h >= 1; h >>= 1) {
+      if (s < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
+      __syncthreads();
+    }
+    if (s == 0 && b < B) bsum[(size_t)slot * B + b] = sh[tid];
+  } else if (b < B) {
+    st_g1r(&bsum[(size_t)slot * B + b], acc);
+  }
+}
+
 // Bucket reduction sum_b (b+1) S_b, split per workgroup g of 256 buckets b = 256g + u,
 // u = 16a + c (a, c < 16):
 //   sum_u (256g + u + 1) S_(g,u) = sum_(j<8) 2^j T_j(g) + (256g + 1) A_g,
@@ -348,8 +378,8 @@ __global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* 
 // j < 4 is a sum of the 8 columns with bit j of c set and T_(4+i) a sum of the 8 rows with
 // bit i of a set; A_g is the sum of the rows: 480 + 71 additions per 256 buckets instead of
 // the 1 144 of bit sums taken over the buckets themselves.
-// k_bitsum1 (one workgroup of 256 lanes per g): the bucket sums S from the accumulation
-// partials, the 32 row / column sums (8 lanes each: one addition, then a 3-level LDS tree),
+// k_bitsum1 (one workgroup of 256 lanes per g): the bucket sums S (k_bucket_sum), the 32
+// row / column sums (8 lanes each: one addition, then a 3-level LDS tree),
 // then the 9 outputs from them (wave 0). out[slot][g][0..7] = T_j(g), [8] = A_g.
 constexpr uint32_t kBitsumOut = 9;
 
@@ -358,21 +388,15 @@ __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
   return ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
 }
 
-__global__ void __launch_bounds__(256) k_bitsum1(const uint32_t* __restrict__ task_off, uint32_t B,
-                                                 uint64_t task_stride,
-                                                 const G1xyzz* __restrict__ partials,
+__global__ void __launch_bounds__(256) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
                                                  G1xyzz* __restrict__ out) {
   __shared__ G1xyzz sh[256 + 32];  // [0, 256): buckets, then tree partials; [256, 288): rows, columns
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
-  task_off += (size_t)slot * (B + 1);
-  partials += (size_t)slot * task_stride;
   out += ((size_t)slot * gridDim.x + g) * kBitsumOut;
   {
     const uint32_t b = g * 256 + tid;
-    G1R acc = g1r_infinity();
-    if (b < B)
-      for (uint32_t t = task_off[b]; t < task_off[b + 1]; ++t) acc = g1r_add(acc, ld_g1r(&partials[t]));
-    st_g1r(&sh[tid], acc);
+    if (b < B) sh[tid] = bsum[(size_t)slot * B + b];
+    else st_g1r(&sh[tid], g1r_infinity());
   }
   __syncthreads();
   {  // sum q < 16: row a = q; q >= 16: column c = q - 16. Lane e of its 8 adds members 2e, 2e + 1.
@@ -439,7 +463,7 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
   }
   st_g1r(&sh[tid], acc);
   __syncthreads();
-  for (uint32_t h = 128; h >= 1; h >>= 1) {
+  for (uint32_t h = min(G, 256u) >> 1; h >= 1; h >>= 1) {  // lanes >= G hold infinity
     if (tid < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
     __syncthreads();
   }
@@ -493,6 +517,7 @@ int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
   if ((st = w.sorted.alloc(slots * (entries + 1) * 4))) return st;
   if ((st = w.tasks.alloc(slots * max_tasks * sizeof(uint2)))) return st;
   if ((st = w.partials.alloc(slots * max_tasks * sizeof(G1xyzz)))) return st;
+  if ((st = w.bsum.alloc(slots * B * sizeof(G1xyzz)))) return st;
   if ((st = w.bits1.alloc(slots * G * kBitsumOut * sizeof(G1xyzz)))) return st;
   if ((st = w.bits2.alloc(slots * 32 * sizeof(G1xyzz)))) return st;  // nbits <= 32
   if ((st = w.flag.alloc(slots * 4 + 16))) return st;
@@ -592,8 +617,19 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
                        s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
   }
   PLK_HIP_TRY(hipEventRecord(w.ev1, stream));
-  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, w.task_off.as<uint32_t>(), B,
-                     (uint64_t)w.task_stride, w.partials.as<G1xyzz>(), w.bits1.as<G1xyzz>());
+  {
+    // lanes per bucket: until each lane adds ~4 partials (partials per bucket = entries /
+    // chunk + 1 tail) or the grid holds 2^17 lanes (the tree levels cost a full addition
+    // per lane, so an already full chip gains nothing from more lanes per bucket)
+    const size_t per_bucket = cdiv(total_entries, (size_t)chunk * B * slots) + 1;
+    uint32_t lp = 0;
+    while (lp < 4 && ((size_t)4 << lp) < per_bucket && (((size_t)B * slots) << lp) < 131072) ++lp;
+    hipLaunchKernelGGL(k_bucket_sum, dim3(cdiv((size_t)B << lp, 256), slots), dim3(256), 0, stream,
+                       w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
+                       w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
+  }
+  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, B, w.bsum.as<G1xyzz>(),
+                     w.bits1.as<G1xyzz>());
   hipLaunchKernelGGL(k_bitsum2, dim3(nbits, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
                      G, nbits, w.bits2.as<G1xyzz>());
   PLK_HIP_TRY(hipGetLastError());

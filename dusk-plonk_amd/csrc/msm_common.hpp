@@ -74,8 +74,8 @@ __device__ __forceinline__ Fr ld_fr(const Fr* p) {
 inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 struct MsmWorkspace {
-  DevBuf counts, blockhist, offsets, task_off, full_off, len_cur, sorted, tasks, partials, bits1, bits2,
-      flag;
+  DevBuf counts, blockhist, offsets, task_off, full_off, len_cur, sorted, tasks, partials, bsum, bits1,
+      bits2, flag;
   PinnedBuf host_out;  // per-slot bit sums T, flags and entry counts read back by the host
   size_t cap_len = 0, task_stride = 0, sorted_stride = 0;
   uint32_t cap_slots = 0;
