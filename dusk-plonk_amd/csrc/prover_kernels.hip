@@ -403,22 +403,18 @@ __global__ void k_lincomb(LinComb lc, Fr* __restrict__ out, uint64_t len_out) {
   stf(&out[j], acc);
 }
 
-// y_j = c_j * x^j (per-thread run of 16: one pow, then successive multiplies)
 // y_j = c_j x^(j + shift). A block covers 256 x 16 consecutive j; the per-thread start
-// powers x^(block start + shift) * (x^16)^t come from an 8-step product scan in LDS.
+// powers x^(block start + shift) * (x^16)^t come from an 8-step product scan in LDS. The
+// host passes x^16, x^4096 and x^shift (one chain of squarings there instead of one per
+// workgroup's first lane, which sat on every launch's critical path).
 __global__ void __launch_bounds__(256) k_scale_powers(const Fr* __restrict__ c, uint64_t len, Fr x,
-                                                      uint64_t shift, Fr* __restrict__ y) {
+                                                      Fr x16, Fr x4096, Fr xshift,
+                                                      Fr* __restrict__ y) {
   __shared__ Fr T[256];
   const uint32_t tid = threadIdx.x;
   const uint64_t jb = (uint64_t)blockIdx.x * 256 * 16;
-  Fr v = x;
-  for (int s = 0; s < 4; ++s) v = fe_sqr(v);  // x^16
-  if (tid == 0) {  // x^(jb + shift), jb = 4096 * blockIdx.x
-    Fr x4096 = v;
-    for (int s = 0; s < 8; ++s) x4096 = fe_sqr(x4096);
-    v = pow_blocks(x4096, blockIdx.x);
-    if (shift) v = fe_mul(v, fe_pow_u64(x, shift));
-  }
+  Fr v = x16;
+  if (tid == 0) v = fe_mul(pow_blocks(x4096, blockIdx.x), xshift);  // x^(jb + shift)
   T[tid] = v;
   __syncthreads();
   for (uint32_t h = 1; h < 256; h <<= 1) {  // inclusive product scan
@@ -547,8 +543,13 @@ int pk_lincomb(const LinComb& lc, Fr* out, uint64_t len_out, hipStream_t s) {
 
 int pk_scale_powers(const Fr* c, uint64_t len, const Fr& x, uint64_t shift, Fr* y, hipStream_t s) {
   if (len == 0) return PLK_OK;
+  Fr x16 = x;
+  for (int i = 0; i < 4; ++i) x16 = fe_sqr(x16);
+  Fr x4096 = x16;
+  for (int i = 0; i < 8; ++i) x4096 = fe_sqr(x4096);
+  const Fr xshift = fe_pow_u64(x, shift);
   hipLaunchKernelGGL(k_scale_powers, dim3(blocks_for((len + 15) / 16, 256)), dim3(256), 0, s, c, len,
-                     x, shift, y);
+                     x, x16, x4096, xshift, y);
   PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
 }
