@@ -37,9 +37,6 @@ namespace plk {
 
 namespace {
 
-#ifndef PLK_XCD_RANK
-#define PLK_XCD_RANK 0
-#endif
 constexpr uint32_t kHistThreads = 1024;
 constexpr uint32_t kHistBlocksMax = 256;  // histogram / scatter workgroups per slot
 
@@ -63,22 +60,9 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, uint32_t c, uin
   return d;
 }
 
-// Rank of this histogram / scatter workgroup among the slot's gridDim.x: workgroups are
-// dispatched round-robin over the 8 XCDs (blockIdx.x % 8), so the ranks of one XCD are made
-// consecutive — their digits land next to each other inside every bucket's segment of the
-// sorted array, and k_scatter's 4-byte writes then share cache lines within one XCD's L2.
-__device__ __forceinline__ uint32_t wg_rank() {
-#if PLK_XCD_RANK
-  const uint32_t n = gridDim.x, x = blockIdx.x;
-  return (n & 7u) ? x : (x & 7u) * (n >> 3) + (x >> 3);
-#else
-  return blockIdx.x;
-#endif
-}
-
 __device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t& i1) {
   const uint32_t per = (len + gridDim.x - 1) / gridDim.x;
-  i0 = wg_rank() * per;
+  i0 = blockIdx.x * per;
   i1 = min(len, i0 + per);
 }
 
@@ -112,7 +96,7 @@ __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cf
   uint32_t i0, i1;
   slot_range(batch.len[slot], i0, i1);
   const Fr* sc = batch.scalars[slot];
-  uint32_t* out = blockhist + ((size_t)slot * gridDim.x + wg_rank()) * B;
+  uint32_t* out = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * B;
   for (uint32_t b0 = 0; b0 < B; b0 += kLdsBuckets) {
     const uint32_t nb = min(kLdsBuckets, B - b0);
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
@@ -227,7 +211,7 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
   const uint32_t slot = blockIdx.y, B = cfg.B;
   const uint32_t* off = offsets + (size_t)slot * (B + 1);
-  const uint32_t* bh = blockhist + ((size_t)slot * gridDim.x + wg_rank()) * B;
+  const uint32_t* bh = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * B;
   uint32_t i0, i1;
   slot_range(batch.len[slot], i0, i1);
   const Fr* sc = batch.scalars[slot];
