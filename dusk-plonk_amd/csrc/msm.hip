@@ -125,8 +125,18 @@ __global__ void k_block_scan(uint32_t* __restrict__ blockhist, uint32_t nblk, ui
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   uint32_t* h = blockhist + (size_t)slot * nblk * B + b;
-  uint32_t run = 0;
-  for (uint32_t k = 0; k < nblk; ++k) {
+  uint32_t run = 0, k = 0;
+  for (; k + 8 <= nblk; k += 8) {  // 8 loads in flight before the stores
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) v[u] = h[(size_t)(k + u) * B];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; ++u) {
+      h[(size_t)(k + u) * B] = run;
+      run += v[u];
+    }
+  }
+  for (; k < nblk; ++k) {
     const uint32_t v = h[(size_t)k * B];
     h[(size_t)k * B] = run;
     run += v;
@@ -246,21 +256,36 @@ __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
                              const uint32_t* __restrict__ full_off, uint32_t* __restrict__ len_cur,
                              uint32_t B, uint32_t chunk, uint2* __restrict__ tasks,
                              uint64_t task_stride) {
-  const uint32_t slot = blockIdx.y;
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  // tails: ranks inside the workgroup from LDS atomics, one global atomic per (workgroup,
+  // length) for the base
+  __shared__ uint32_t s_cnt[kChunkMax], s_base[kChunkMax];
+  const uint32_t slot = blockIdx.y, tid = threadIdx.x;
+  const uint32_t b = blockIdx.x * blockDim.x + tid;
+  for (uint32_t l = tid; l < kChunkMax; l += blockDim.x) s_cnt[l] = 0;
+  __syncthreads();
   offsets += (size_t)slot * (B + 1);
   task_off += (size_t)slot * (B + 1);
   tasks += (size_t)slot * task_stride;
-  const uint32_t start = offsets[b], cnt = offsets[b + 1] - start;
-  const uint32_t t0 = task_off[b], nfull = cnt / chunk;
+  uint32_t start = 0, t0 = 0, nfull = 0, tail = 0, rank = 0;
+  if (b < B) {
+    start = offsets[b];
+    const uint32_t cnt = offsets[b + 1] - start;
+    t0 = task_off[b];
+    nfull = cnt / chunk;
+    tail = cnt - nfull * chunk;
+    if (tail) rank = atomicAdd(&s_cnt[tail], 1u);
+  }
+  __syncthreads();
+  for (uint32_t l = tid; l < kChunkMax; l += blockDim.x)
+    if (s_cnt[l]) s_base[l] = atomicAdd(&len_cur[(size_t)slot * kChunkMax + l], s_cnt[l]);
+  __syncthreads();
+  if (b >= B) return;
   uint32_t x = full_off[(size_t)slot * B + b];
   for (uint32_t t = 0; t < nfull; ++t, ++x)
     tasks[x] = make_uint2(start + t * chunk, (t0 + t) | ((chunk - 1) << kTaskShift));
-  if (const uint32_t tail = cnt - nfull * chunk) {
-    const uint32_t e = atomicAdd(&len_cur[(size_t)slot * kChunkMax + tail], 1u);
-    tasks[e] = make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << kTaskShift));
-  }
+  if (tail)
+    tasks[s_base[tail] + rank] =
+        make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << kTaskShift));
 }
 
 #ifndef PLK_ACC_WAVES

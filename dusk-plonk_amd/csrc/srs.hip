@@ -99,7 +99,10 @@ static uint32_t choose_c(size_t n) {
 #define PLK_C_LARGE 16  // 17 (15 windows) measured slower end to end: its 2x buckets cost more in the sort and reduction kernels than the 6% fewer entries save
 #endif
   if (n >= (1u << 18)) return PLK_C_LARGE;
-  if (n >= (1u << 14)) return 13;
+#ifndef PLK_C_MID
+#define PLK_C_MID 13
+#endif
+  if (n >= (1u << 14)) return PLK_C_MID;
   if (n >= (1u << 10)) return 10;
   return 8;
 }

@@ -12,7 +12,7 @@ summ='import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e
 for k in 20 16; do
   for v in default "$@"; do
     if [ "$v" = default ]; then lib=""; else lib="$PWD/dusk-plonk_amd/libplk-$v.so"; fi
-    PLK_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --log-n $k > $d/bench_${v}_$k.log 2>&1 || { echo BENCH_FAILED $v; tail -20 $d/bench_${v}_$k.log; exit 1; }
+    PLK_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --log-n $k $( [ $k = 16 ] && echo "--steps 20 --warmup 3" ) > $d/bench_${v}_$k.log 2>&1 || { echo BENCH_FAILED $v; tail -20 $d/bench_${v}_$k.log; exit 1; }
     echo -n "2^$k $v: "; grep '"metric"' $d/bench_${v}_$k.log | python3 -c "$summ"
   done
 done
