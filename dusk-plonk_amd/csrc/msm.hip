@@ -37,6 +37,12 @@ namespace plk {
 
 namespace {
 
+#ifndef PLK_LANE_PARTIALS
+#define PLK_LANE_PARTIALS 8  // bucket partials per k_bucket_sum lane aimed at (4: +0.1 ms per proof)
+#endif
+#ifndef PLK_CHUNK_TARGET
+#define PLK_CHUNK_TARGET 262144  // accumulation tasks aimed at per batch (chunk = entries / this)
+#endif
 constexpr uint32_t kHistThreads = 1024;
 constexpr uint32_t kHistBlocksMax = 256;  // histogram / scatter workgroups per slot
 
@@ -575,7 +581,7 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
   const uint32_t slots = (uint32_t)count;
   // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads
   const uint32_t chunk = (uint32_t)std::min<size_t>(
-      kChunkMax, std::max<size_t>(kChunkMin, total_entries / 262144));
+      kChunkMax, std::max<size_t>(kChunkMin, total_entries / PLK_CHUNK_TARGET));
   const size_t max_tasks_used = (size_t)s->windows * max_len / chunk + B;
   // 256 workgroups per slot: fewer give longer per-bucket write runs in k_scatter but lose
   // more parallelism than they gain (measured 2.77 / 2.79 / 3.02 / 4.52 ms per proof at
@@ -627,12 +633,12 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
   }
   PLK_HIP_TRY(hipEventRecord(w.ev1, stream));
   {
-    // lanes per bucket: until each lane adds ~4 partials (partials per bucket = entries /
+    // lanes per bucket: until each lane adds ~PLK_LANE_PARTIALS partials (partials per bucket = entries /
     // chunk + 1 tail) or the grid holds 2^17 lanes (the tree levels cost a full addition
     // per lane, so an already full chip gains nothing from more lanes per bucket)
     const size_t per_bucket = cdiv(total_entries, (size_t)chunk * B * slots) + 1;
     uint32_t lp = 0;
-    while (lp < 4 && ((size_t)4 << lp) < per_bucket && (((size_t)B * slots) << lp) < 131072) ++lp;
+    while (lp < 4 && ((size_t)PLK_LANE_PARTIALS << lp) < per_bucket && (((size_t)B * slots) << lp) < 131072) ++lp;
     hipLaunchKernelGGL(k_bucket_sum, dim3(cdiv((size_t)B << lp, 256), slots), dim3(256), 0, stream,
                        w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
                        w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
