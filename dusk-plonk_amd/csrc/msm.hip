@@ -357,8 +357,8 @@ __global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* 
 
 // Bucket sums S_b = sum of bucket b's accumulation partials (task_off[b] .. task_off[b+1]):
 // 2^lp lanes per bucket, each adding every 2^lp-th partial, then an LDS tree over the lanes
-// (2^lp is sized on the host to the partials per bucket, so the sequential chain stays ~4
-// additions at every MSM size).
+// (2^lp is sized on the host to the partials per bucket, so the sequential chain stays
+// ~PLK_LANE_PARTIALS additions at every MSM size, unless the grid is already full).
 __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__ task_off,
                                                     uint32_t B, uint32_t lp, uint64_t task_stride,
                                                     const G1xyzz* __restrict__ partials,
