@@ -53,11 +53,15 @@ def parse():
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--lanes", type=int, default=3,
+    ap.add_argument("--lanes", type=int, default=0,
                     help="concurrent prover lanes per GPU (prove mode): independent contexts "
-                         "with their own streams, each driven by a host thread (sweep, "
-                         "tools/gpu_lanes*.sh: 2^20 17.6/20.2/20.9/20.8 M and 2^16 "
-                         "6.0/9.3/11.3/10.3/11.4 M constraints/s at 1/2/3/4(/6) lanes)")
+                         "with their own streams, each driven by a host thread. 0 = 8 at "
+                         "n >= 2^18, 12 below (tools/gpu_queues.sh with 2 HIP hardware queues "
+                         "per lane: 2^20 23.5/24.1/24.4/24.2 M and 2^16 14.9/17.0/17.3/18.6 M "
+                         "constraints/s at 3/6/8/12 lanes)")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4); "
+                         "0 = min(32, 2 x lanes): more lanes than queues serialise on them")
     ap.add_argument("--mode", choices=["prove", "hotpath"], default="prove",
                     help="prove: full Prover::create_proof (synthesis + 5 rounds + openings); "
                          "hotpath: only the 19 NTTs + 11 MSMs of one proof")
@@ -415,6 +419,7 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
             "n": n, "log_n": k, "proofs_per_step": world * L,
             "parallelism": f"proof-batch x{world * L} ({L} concurrent prover lane(s) per GPU)",
             "msm_window_bits": cbits,
+            "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
         },
         "breakdown_ms_per_step": {
             "synthesis_host_overlapped": 1e3 * sum(sum(l.synth_s) for l in lanes) / (steps * L),
@@ -450,6 +455,13 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
 
 def main():
     args = parse()
+    if args.lanes <= 0:
+        args.lanes = 8 if args.log_n >= 18 else 12
+    if args.mode == "prove":
+        # before the HIP runtime starts (the torch import below): each lane's stream gets a
+        # hardware queue of its own
+        q = args.hw_queues or min(32, 2 * args.lanes)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, q))
     import torch
     import torch.distributed as dist
 
