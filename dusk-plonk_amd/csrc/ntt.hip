@@ -63,6 +63,12 @@ __device__ __forceinline__ void lds_st(uint32_t* base, uint32_t stride, uint32_t
 
 __device__ __forceinline__ RFr ld_rfr(const Fr* p) { return rx_unpack(ld_fr(p)); }
 
+// a - b + 3r limb by limb, no carries (9 instructions against 27 for rx_sub_lazy; a, b
+// normalised below 2r): limbs below 2^29 + 2^30, value in (r, 5r). Only as a multiplicand
+// of a normalised twiddle: columns 9 * 2^60 + 9 * 2^58 < 2^64, product 10r^2 / R' + r < 2r
+// (ffr.hpp rx_sub_u, R' / r > 70).
+__device__ __forceinline__ RFr sub_u(const RFr& a, const RFr& b) { return rx_sub_u<FrCfg, 3>(a, b); }
+
 // One Stockham pass. PRE: 0 none, 1 multiply input e by pre[e] (coset g^e).
 // POST: 0 none, 1 multiply by post_scalar, 2 multiply output e by post[e].
 // Data buffers are R-domain (canonical in and out); tw / pre / post / post_scalar are
@@ -164,15 +170,15 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       const RFr x2 = lds_ld(data, E, i2), x3 = lds_ld(data, E, i3);
       // stage of half 2h: twiddle w^(r s1) for x0/x2 (identity when r = 0), w^((r+h) s1)
       const RFr y0 = rx_add(x0, x2), y1 = rx_add(x1, x3);
-      const RFr y2 = r != 0 ? rx_mul(rx_sub_lazy(x0, x2), lds_ld(twl, TS, r << sh1)) : rx_sub(x0, x2);
-      const RFr y3 = rx_mul(rx_sub_lazy(x1, x3), lds_ld(twl, TS, (r + h) << sh1));
+      const RFr y2 = r != 0 ? rx_mul(sub_u(x0, x2), lds_ld(twl, TS, r << sh1)) : rx_sub(x0, x2);
+      const RFr y3 = rx_mul(sub_u(x1, x3), lds_ld(twl, TS, (r + h) << sh1));
       // stage of half h: twiddle w^(r s2) for both pairs
       lds_st(data, E, i0, rx_add(y0, y1));
       lds_st(data, E, i2, rx_add(y2, y3));
       if (r != 0) {
         const RFr w = lds_ld(twl, TS, r << sh2);
-        lds_st(data, E, i1, rx_mul(rx_sub_lazy(y0, y1), w));
-        lds_st(data, E, i3, rx_mul(rx_sub_lazy(y2, y3), w));
+        lds_st(data, E, i1, rx_mul(sub_u(y0, y1), w));
+        lds_st(data, E, i3, rx_mul(sub_u(y2, y3), w));
       } else {
         lds_st(data, E, i1, rx_sub(y0, y1));
         lds_st(data, E, i3, rx_sub(y2, y3));
