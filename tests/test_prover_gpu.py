@@ -117,8 +117,10 @@ def test_proofs_are_deterministic_per_seed(plk):
     assert p1.to_bytes() != p3.to_bytes()
 
 
-@pytest.mark.parametrize("logn", [6, 10, 12])
+@pytest.mark.parametrize("logn", [6, 10, 12, 16, 20])
 def test_chain_circuit_proves_and_verifies(plk, logn):
+    """Including the benchmark's own sizes (2^16 and 2^20: c = 13 / 16 windows, pruned
+    first NTT passes, multi-lane bucket sums): a fresh-witness proof the verifier accepts."""
     from dusk_plonk_amd.prover import PlonkKey
     tau, pp = tau_and_params(plk, logn, logn)
     gates = (1 << logn) - 8 - 6
