@@ -328,6 +328,16 @@ __device__ __forceinline__ Fr pow_blocks(Fr x4096, uint64_t b) {
   return r;
 }
 
+// the same in the R' domain of ffr.hpp (x4096 and the result R'-domain, [0, 2r))
+__device__ __forceinline__ RFr pow_blocks_rx(RFr x4096, uint64_t b) {
+  RFr r = rx_one<FrCfg>();
+  for (; b; b >>= 1) {
+    if (b & 1) r = rx_mul(r, x4096);
+    x4096 = rx_sqr(x4096);
+  }
+  return r;
+}
+
 // partial[k][blk] = sum_{j in block} c_j x^j (poly k of the batch). Thread t runs Horner
 // in x^256 over c_{block + t + 256 i}, i < kEvalPer (consecutive threads read consecutive
 // coefficients: coalesced), giving H_t with sum_j c_j x^j = sum_t x^t H_t; the workgroup
@@ -335,44 +345,48 @@ __device__ __forceinline__ Fr pow_blocks(Fr x4096, uint64_t b) {
 // power x^(block start) per block (pow_blocks).
 __global__ void __launch_bounds__(kEvalThreads) k_eval_partial(EvalBatch e, Fr* __restrict__ partial,
                                                                uint32_t max_blocks) {
+  // redundant-limb arithmetic: coefficients R-domain, powers of x R'-domain (the host
+  // converts e.x), so every product lands in the R domain; LDS holds packed [0, 2r) values
   __shared__ Fr sh[kEvalThreads];
-  __shared__ Fr xp[9];  // x^(2^l), l = 0..8 (x^256 last)
+  __shared__ Fr xp[9];  // x^(2^l), l = 0..8 (x^256 last), R'
   __shared__ Fr xblock;
   const uint32_t k = blockIdx.y, tid = threadIdx.x;
   const Fr* p = e.poly[k];
   const uint64_t len = e.len[k];
-  const Fr x = e.x[k];
   const uint64_t block0 = (uint64_t)blockIdx.x * kEvalBlock;
   if (block0 >= len) {  // whole block past this polynomial's end (uniform per block)
     if (tid == 0) stf(&partial[(size_t)k * max_blocks + blockIdx.x], fe_zero<FrCfg>());
     return;
   }
   if (tid == 0) {
-    Fr t = x;
+    RFr t = rx_unpack(e.x[k]);
     for (int l = 0; l < 9; ++l) {
-      xp[l] = t;
-      t = fe_sqr(t);
+      xp[l] = rx_pack(t);
+      t = rx_sqr(t);
     }
-    for (int l = 9; l < 12; ++l) t = fe_sqr(t);  // x^4096
-    xblock = pow_blocks(t, blockIdx.x);
+    for (int l = 9; l < 12; ++l) t = rx_sqr(t);  // x^4096
+    xblock = rx_pack(pow_blocks_rx(t, blockIdx.x));
   }
   __syncthreads();
-  const Fr x256 = xp[8];
-  Fr acc = fe_zero<FrCfg>();
+  const RFr x256 = rx_unpack(xp[8]);
+  RFr acc = rx_zero<FrCfg>();
 #pragma unroll
   for (int i = (int)kEvalPer - 1; i >= 0; --i) {
     const uint64_t j = block0 + tid + (uint64_t)i * kEvalThreads;
-    acc = fe_mul(acc, x256);
-    if (j < len) acc = fe_add(acc, ldf(&p[j]));
+    acc = rx_mul(acc, x256);
+    if (j < len) acc = rx_add(acc, ldr(&p[j]));
   }
-  sh[tid] = acc;
+  sh[tid] = rx_pack(acc);
   __syncthreads();
   for (int l = 7; l >= 0; --l) {
     const uint32_t h = 1u << l;
-    if (tid < h) sh[tid] = fe_add(sh[tid], fe_mul(sh[tid + h], xp[l]));
+    if (tid < h)
+      sh[tid] = rx_pack(rx_add(rx_unpack(sh[tid]), rx_mul(rx_unpack(sh[tid + h]), rx_unpack(xp[l]))));
     __syncthreads();
   }
-  if (tid == 0) stf(&partial[(size_t)k * max_blocks + blockIdx.x], fe_mul(sh[0], xblock));
+  if (tid == 0)
+    stf(&partial[(size_t)k * max_blocks + blockIdx.x],
+        rx_pack_canonical(rx_mul(rx_unpack(sh[0]), rx_unpack(xblock))));
 }
 
 __global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restrict__ partial,
@@ -394,13 +408,14 @@ __global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restric
 
 // ---------------------------------------------------------------- linear combos
 // out[j] = sum_t s_t * p_t[j] (p_t[j] = 0 past len_t), j < len_out
+// (redundant limbs: the scalars arrive in the R' domain, pk_lincomb)
 __global__ void k_lincomb(LinComb lc, Fr* __restrict__ out, uint64_t len_out) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= len_out) return;
-  Fr acc = fe_zero<FrCfg>();
+  RFr acc = rx_zero<FrCfg>();
   for (uint32_t t = 0; t < lc.terms; ++t)
-    if (j < lc.len[t]) acc = fe_add(acc, fe_mul(lc.s[t], ldf(&lc.p[t][j])));
-  stf(&out[j], acc);
+    if (j < lc.len[t]) acc = rx_add(acc, rx_mul(rx_unpack(lc.s[t]), ldr(&lc.p[t][j])));
+  stf(&out[j], rx_pack_canonical(acc));
 }
 
 // y_j = c_j x^(j + shift). A block covers 256 x 16 consecutive j; the per-thread start
@@ -528,7 +543,9 @@ int pk_scale_copy(const Fr* in, const Fr& c, Fr* out, uint64_t n, hipStream_t s)
 int pk_eval(const EvalBatch& e, uint32_t count, uint64_t max_len, Fr* partial, Fr* d_out,
             hipStream_t s) {
   const uint32_t mb = pk_eval_max_blocks(max_len ? max_len : 1);
-  hipLaunchKernelGGL(k_eval_partial, dim3(mb, count), dim3(kEvalThreads), 0, s, e, partial, mb);
+  EvalBatch er = e;  // evaluation points in the R' domain (k_eval_partial)
+  for (uint32_t k = 0; k < count; ++k) er.x[k] = fe_to_rx_domain(e.x[k]);
+  hipLaunchKernelGGL(k_eval_partial, dim3(mb, count), dim3(kEvalThreads), 0, s, er, partial, mb);
   hipLaunchKernelGGL(k_eval_final, dim3(count), dim3(kEvalThreads), 0, s, partial, mb, mb, d_out);
   PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
@@ -536,7 +553,9 @@ int pk_eval(const EvalBatch& e, uint32_t count, uint64_t max_len, Fr* partial, F
 
 int pk_lincomb(const LinComb& lc, Fr* out, uint64_t len_out, hipStream_t s) {
   if (len_out == 0) return PLK_OK;
-  hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(len_out, 256)), dim3(256), 0, s, lc, out, len_out);
+  LinComb lr = lc;  // scalars in the R' domain (k_lincomb)
+  for (uint32_t t = 0; t < lc.terms; ++t) lr.s[t] = fe_to_rx_domain(lc.s[t]);
+  hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(len_out, 256)), dim3(256), 0, s, lr, out, len_out);
   PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
 }
