@@ -24,6 +24,7 @@
 //  * Up to kMaxSlots independent MSMs run as ONE batch (blockIdx.y = slot): the prover's
 //    commits come in independent groups (4 wires, 4 quotient chunks, 2 openings), and the
 //    latency-bound tail kernels of a batch then cost about what one MSM's tail costs.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -617,21 +618,25 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
                      w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),
                      w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>(), B, chunk,
                      w.tasks.as<uint2>(), (uint64_t)w.task_stride);
-  PLK_HIP_TRY(hipEventRecord(w.ev0, stream));
-  if (s->has_inf) {
-    hipLaunchKernelGGL(k_accumulate<true>, dim3(cdiv(max_tasks_used, 256), slots), dim3(256), 0,
-                       stream, w.tasks.as<uint2>(), w.task_off.as<uint32_t>(), B,
-                       (uint64_t)w.task_stride, w.sorted.as<uint32_t>(),
-                       (uint64_t)w.sorted_stride, s->table.as<G1Affine>(),
-                       s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
-  } else {
-    hipLaunchKernelGGL(k_accumulate<false>, dim3(cdiv(max_tasks_used, 256), slots), dim3(256), 0,
-                       stream, w.tasks.as<uint2>(), w.task_off.as<uint32_t>(), B,
-                       (uint64_t)w.task_stride, w.sorted.as<uint32_t>(),
-                       (uint64_t)w.sorted_stride, s->table.as<G1Affine>(),
-                       s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
+  // start / stop events stamped by the dispatch itself (its execution, as rocprofv3 times
+  // it), not by the stream: with several lanes on the GPU a stream event would also count
+  // the time the kernel waits behind other lanes' kernels
+  {
+    const dim3 grid(cdiv(max_tasks_used, 256), slots), block(256);
+    if (s->has_inf) {
+      hipExtLaunchKernelGGL(k_accumulate<true>, grid, block, 0, stream, w.ev0, w.ev1, 0,
+                            (const uint2*)w.tasks.as<uint2>(), (const uint32_t*)w.task_off.as<uint32_t>(),
+                            B, (uint64_t)w.task_stride, (const uint32_t*)w.sorted.as<uint32_t>(),
+                            (uint64_t)w.sorted_stride, (const G1Affine*)s->table.as<G1Affine>(),
+                            (const uint8_t*)s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
+    } else {
+      hipExtLaunchKernelGGL(k_accumulate<false>, grid, block, 0, stream, w.ev0, w.ev1, 0,
+                            (const uint2*)w.tasks.as<uint2>(), (const uint32_t*)w.task_off.as<uint32_t>(),
+                            B, (uint64_t)w.task_stride, (const uint32_t*)w.sorted.as<uint32_t>(),
+                            (uint64_t)w.sorted_stride, (const G1Affine*)s->table.as<G1Affine>(),
+                            (const uint8_t*)s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
+    }
   }
-  PLK_HIP_TRY(hipEventRecord(w.ev1, stream));
   {
     // lanes per bucket: until each lane adds ~PLK_LANE_PARTIALS partials (partials per bucket = entries /
     // chunk + 1 tail) or the grid holds 2^17 lanes (the tree levels cost a full addition
