@@ -38,6 +38,30 @@ __device__ __forceinline__ void stf(Fr* p, const Fr& v) {
 using RFr = Rx<FrCfg>;
 __device__ __forceinline__ RFr ldr(const Fr* p) { return rx_unpack(ldf(p)); }
 
+// a + b + c limb by limb, no carries (a, b, c normalised, each below 2r): limbs below
+// 3 * 2^29, value below 6r. Only as a multiplicand of a normalised operand below 6r: columns
+// 9 * 1.5 * 2^59 + 9 * 2^58 < 2^64, product 36 r^2 / R' + r < 2r (R' / r > 70).
+__device__ __forceinline__ RFr add3_u(const RFr& a, const RFr& b, const RFr& c) {
+  RFr r;
+#pragma unroll
+  for (int l = 0; l < RxShape<FrCfg>::L; ++l) r.v[l] = a.v[l] + b.v[l] + c.v[l];
+  return r;
+}
+
+// carries propagated: normalised limbs, same value
+__device__ __forceinline__ RFr rx_norm(const RFr& a) {
+  constexpr uint32_t B = RxShape<FrCfg>::B, MASK = (1u << B) - 1;
+  RFr r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int l = 0; l < RxShape<FrCfg>::L; ++l) {
+    const uint32_t t = a.v[l] + c;
+    r.v[l] = l == RxShape<FrCfg>::L - 1 ? t : (t & MASK);
+    c = t >> B;
+  }
+  return r;
+}
+
 inline uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
 // ---------------------------------------------------------------------------- wires
@@ -234,15 +258,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
   const RFr bX2 = rx_dbl(bX), bX4 = rx_dbl(bX2), bX8 = rx_dbl(bX4), bX16 = rx_dbl(bX8);
   const RFr bX7 = rx_sub(bX8, bX), bX13 = rx_add(rx_add(bX8, bX4), bX), bX17 = rx_add(bX16, bX);
   const RFr gm = rx_unpack(q.rx_gamma);  // [-1]
-  RFr id = rx_mul(rx_add(rx_add(a, bX), gm), rx_add(rx_add(b, bX7), gm));
-  id = rx_mul(id, rx_add(rx_add(c, bX13), gm));
-  id = rx_mul(id, rx_add(rx_add(d, bX17), gm));
+  // the factors are carry-free sums (add3_u), each multiplied by a normalised operand
+  RFr id = rx_mul(rx_norm(add3_u(a, bX, gm)), add3_u(b, bX7, gm));
+  id = rx_mul(id, add3_u(c, bX13, gm));
+  id = rx_mul(id, add3_u(d, bX17, gm));
   id = rx_mul(id, z);  // [0]
   const RFr be = rx_unpack(q.rx_beta);  // [-2]
-  RFr cp = rx_add(rx_add(a, rx_mul(be, ldr(&q.sigma[0 * N + i]))), gm);
-  cp = rx_mul(cp, rx_add(rx_add(b, rx_mul(be, ldr(&q.sigma[1 * N + i]))), gm));
-  cp = rx_mul(cp, rx_add(rx_add(c, rx_mul(be, ldr(&q.sigma[2 * N + i]))), gm));
-  cp = rx_mul(cp, rx_add(rx_add(d, rx_mul(be, ldr(&q.sigma[3 * N + i]))), gm));
+  RFr cp = rx_norm(add3_u(a, rx_mul(be, ldr(&q.sigma[0 * N + i])), gm));
+  cp = rx_mul(cp, add3_u(b, rx_mul(be, ldr(&q.sigma[1 * N + i])), gm));
+  cp = rx_mul(cp, add3_u(c, rx_mul(be, ldr(&q.sigma[2 * N + i])), gm));
+  cp = rx_mul(cp, add3_u(d, rx_mul(be, ldr(&q.sigma[3 * N + i])), gm));
   cp = rx_mul(cp, z_next);  // [0]
   RFr perm = rx_mul(rx_sub(id, cp), rx_unpack(q.alpha));  // [1]
   // alpha^2 L1(X): coset_dft is linear, so alpha^2 * coset_dft(idft(e_0)) equals the
