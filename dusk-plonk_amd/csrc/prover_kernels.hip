@@ -224,13 +224,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
   const RFr a = ldr(&q.a[i]), b = ldr(&q.b[i]), c = ldr(&q.c[i]), d = ldr(&q.d[i]);
   const RFr z = ldr(&q.z[i]), z_next = ldr(&q.z[nx]);
   // arithmetic widget: q_arith (q_m a b + q_l a + q_r b + q_o c + q_4 d + q_c), terms [0]
+  // (pairs of products share one reduction, rx_mul_add; the four terms summed carry-free:
+  // limbs below 2^31, value below 8r, times the normalised q_arith: 16 r^2 / R' + r < 2r)
   RFr t = rx_mul(ldr(&q.sel[SEL_QM * N + i]), rx_mul(a, b));
-  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_QL * N + i]), a));
-  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_QR * N + i]), b));
-  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_QO * N + i]), c));
-  t = rx_add(t, rx_mul(ldr(&q.sel[SEL_Q4 * N + i]), d));
-  t = rx_add(t, ldr(&q.sel[SEL_QC * N + i]));
-  t = rx_mul(t, ldr(&q.sel[SEL_QARITH * N + i]));  // [1]
+  const RFr lr = rx_mul_add(ldr(&q.sel[SEL_QL * N + i]), a, ldr(&q.sel[SEL_QR * N + i]), b);
+  const RFr o4 = rx_mul_add(ldr(&q.sel[SEL_QO * N + i]), c, ldr(&q.sel[SEL_Q4 * N + i]), d);
+  const RFr qc = ldr(&q.sel[SEL_QC * N + i]);
+#pragma unroll
+  for (int l = 0; l < RxShape<FrCfg>::L; ++l) t.v[l] += lr.v[l] + o4.v[l] + qc.v[l];
+  t = rx_mul(ldr(&q.sel[SEL_QARITH * N + i]), t);  // [1]
   if (q.pi) t = rx_add(t, ldr(&q.pi[i]));           // public inputs arrive at [1]
   // range widget: sep * q_range * (D(c-4d) + D(b-4c) k + D(a-4b) k^2 + D(d_next-4a) k^3)
   if (q.has_range) {
