@@ -271,13 +271,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
   cp = rx_mul(cp, add3_u(c, rx_mul(be, ldr(&q.sigma[2 * N + i])), gm));
   cp = rx_mul(cp, add3_u(d, rx_mul(be, ldr(&q.sigma[3 * N + i])), gm));
   cp = rx_mul(cp, z_next);  // [0]
-  RFr perm = rx_mul(rx_sub(id, cp), rx_unpack(q.alpha));  // [1]
   // alpha^2 L1(X): coset_dft is linear, so alpha^2 * coset_dft(idft(e_0)) equals the
-  // reference's coset_dft(idft(alpha^2 e_0)) exactly
-  const RFr zm1 = rx_sub(z, rx_unpack(fe_one<FrCfg>()));
-  perm = rx_add(perm, rx_mul(rx_mul(zm1, ldr(&q.l1[i])), rx_unpack(q.rx_alpha2)));  // [1]
-  const RFr num = rx_add(t, perm);                                                    // [1]
-  stf(&q.out[i], rx_pack_canonical(FINAL ? rx_mul(num, rx_unpack(q.rx_vh[i & 7])) : num));
+  // reference's coset_dft(idft(alpha^2 e_0)) exactly. alpha (id - cp) + alpha^2 (z - 1) L1
+  // with one reduction: (id - cp + 3r) carry-free, (5r * 2r + 2r * 2r) / R' + r < 2r
+  const RFr zm1l1 = rx_mul(rx_sub_u<FrCfg, 3>(z, rx_unpack(fe_one<FrCfg>())), ldr(&q.l1[i]));
+  const RFr perm = rx_mul_add(rx_sub_u<FrCfg, 3>(id, cp), rx_unpack(q.alpha), zm1l1,
+                              rx_unpack(q.rx_alpha2));  // [1]
+  if (FINAL) {  // t + perm carry-free (below 4r) times the normalised 1 / v_h
+    RFr num = t;
+#pragma unroll
+    for (int l = 0; l < RxShape<FrCfg>::L; ++l) num.v[l] += perm.v[l];
+    stf(&q.out[i], rx_pack_canonical(rx_mul(num, rx_unpack(q.rx_vh[i & 7]))));
+  } else {
+    stf(&q.out[i], rx_pack_canonical(rx_add(t, perm)));  // [1]
+  }
 }
 
 // out[i] = (out[i] + logic + fixed-base + variable-base terms) / v_h
