@@ -88,24 +88,32 @@ __global__ void k_fill(Fr* __restrict__ out, Fr v, uint64_t n) {
 
 // ------------------------------------------------------------------- grand product
 // num_i = prod_c (w_c + beta k_c w^i + gamma), den_i = prod_c (w_c + beta sigma_c + gamma)
+// Redundant limbs: beta and k_c arrive in the R' domain, so beta x and k_c beta x are
+// R-domain like the wires and gamma; the factors are carry-free sums (add3_u); a product
+// of four R-domain factors is R^4 / R'^3 times the value, and `fix` = R'^4 / R^3 mod r
+// (a plain integer) brings it back to R.
 __global__ void k_perm_numden(const Fr* __restrict__ wires, const Fr* __restrict__ sigmas,
-                              const Fr* __restrict__ elements, uint64_t n, Fr beta, Fr gamma,
-                              Fr k1, Fr k2, Fr k3, Fr* __restrict__ num, Fr* __restrict__ den) {
+                              const Fr* __restrict__ elements, uint64_t n, Fr beta_rx, Fr gamma,
+                              Fr k1_rx, Fr k2_rx, Fr k3_rx, Fr fix, Fr* __restrict__ num,
+                              Fr* __restrict__ den) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const Fr x = ldf(&elements[i]);
-  const Fr bx = fe_mul(beta, x);
-  const Fr ks[4] = {fe_one<FrCfg>(), k1, k2, k3};
-  Fr nu = fe_one<FrCfg>(), de = fe_one<FrCfg>();
+  const RFr be = rx_unpack(beta_rx), g = rx_unpack(gamma);
+  const RFr bx = rx_mul(be, ldr(&elements[i]));
+  const RFr bxk[4] = {bx, rx_mul(rx_unpack(k1_rx), bx), rx_mul(rx_unpack(k2_rx), bx),
+                      rx_mul(rx_unpack(k3_rx), bx)};
+  RFr nu, de;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    const Fr w = ldf(&wires[c * n + i]);
-    const Fr wg = fe_add(w, gamma);
-    nu = fe_mul(nu, fe_add(wg, c == 0 ? bx : fe_mul(ks[c], bx)));
-    de = fe_mul(de, fe_add(wg, fe_mul(beta, ldf(&sigmas[c * n + i]))));
+    const RFr w = ldr(&wires[c * n + i]);
+    const RFr tn = add3_u(w, g, bxk[c]);
+    const RFr td = add3_u(w, g, rx_mul(be, ldr(&sigmas[c * n + i])));
+    nu = c == 0 ? rx_norm(tn) : rx_mul(nu, tn);
+    de = c == 0 ? rx_norm(td) : rx_mul(de, td);
   }
-  stf(&num[i], nu);
-  stf(&den[i], de);
+  const RFr f = rx_unpack(fix);
+  stf(&num[i], rx_pack_canonical(rx_mul(nu, f)));
+  stf(&den[i], rx_pack_canonical(rx_mul(de, f)));
 }
 
 // z_i = N_i * S_i * dinv
@@ -508,8 +516,12 @@ int pk_fill(Fr* out, const Fr& v, uint64_t n, hipStream_t s) {
 int pk_perm_numden(const Fr* wires, const Fr* sigmas, const Fr* elements, uint64_t n,
                    const Fr& beta, const Fr& gamma, const Fr& k1, const Fr& k2, const Fr& k3,
                    Fr* num, Fr* den, hipStream_t s) {
+  Fr fix = fe_zero<FrCfg>();  // 2^276 mod r = R'^4 / R^3 (k_perm_numden)
+  fix.v[0] = 1;
+  for (int b = 0; b < 4 * RxShape<FrCfg>::B * RxShape<FrCfg>::L - 3 * 256; ++b) fix = fe_dbl(fix);
   hipLaunchKernelGGL(k_perm_numden, dim3(blocks_for(n, 256)), dim3(256), 0, s, wires, sigmas,
-                     elements, n, beta, gamma, k1, k2, k3, num, den);
+                     elements, n, fe_to_rx_domain(beta), gamma, fe_to_rx_domain(k1),
+                     fe_to_rx_domain(k2), fe_to_rx_domain(k3), fix, num, den);
   PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
 }
