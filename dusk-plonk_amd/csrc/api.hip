@@ -5,7 +5,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <algorithm>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "internal.hpp"
@@ -425,6 +427,37 @@ int plk_g1_sum(const plk_g1* points, size_t n, plk_g1* out) {
   const bool fin = xyzz_to_affine(acc, r.x, r.y);
   g1_to_abi(r, fin ? 0 : 1, out);
   return PLK_OK;
+  PLK_API_END
+}
+
+int plk_msm_sharded(plk_srs* const* per_gpu, int n_gpu, const plk_fr* scalars, size_t len,
+                    plk_g1* out) {
+  PLK_API_BEGIN
+  if (!per_gpu || n_gpu <= 0 || !out || (!scalars && len)) return PLK_E_ARG;
+  size_t total = 0;
+  for (int i = 0; i < n_gpu; ++i) {
+    if (!per_gpu[i]) return PLK_E_ARG;
+    total += per_gpu[i]->n;
+  }
+  if (len > total) return PLK_E_ARG;
+  std::vector<plk_g1> part((size_t)n_gpu, plk_g1{});
+  std::vector<int> status((size_t)n_gpu, PLK_OK);
+  std::vector<std::thread> workers;
+  size_t off = 0;
+  for (int i = 0; i < n_gpu; ++i) {
+    plk_srs* s = per_gpu[i];
+    const size_t cnt = off < len ? std::min(s->n, len - off) : 0;
+    part[i].infinity = 1;
+    if (cnt)
+      workers.emplace_back([&part, &status, s, i, cnt, p = scalars + off]() {
+        status[i] = plk_msm(s, p, cnt, &part[i]);
+      });
+    off += s->n;
+  }
+  for (auto& t : workers) t.join();
+  for (int i = 0; i < n_gpu; ++i)
+    if (status[i] != PLK_OK) return status[i];
+  return plk_g1_sum(part.data(), (size_t)n_gpu, out);
   PLK_API_END
 }
 

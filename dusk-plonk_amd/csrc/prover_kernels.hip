@@ -467,26 +467,29 @@ __global__ void k_lincomb(LinComb lc, Fr* __restrict__ out, uint64_t len_out) {
 __global__ void __launch_bounds__(256) k_scale_powers(const Fr* __restrict__ c, uint64_t len, Fr x,
                                                       Fr x16, Fr x4096, Fr xshift,
                                                       Fr* __restrict__ y) {
+  // redundant limbs: the powers live in the R' domain (the host converts x, x^16, x^4096
+  // and x^shift), so c_j x^j lands in the R domain of c
   __shared__ Fr T[256];
   const uint32_t tid = threadIdx.x;
   const uint64_t jb = (uint64_t)blockIdx.x * 256 * 16;
-  Fr v = x16;
-  if (tid == 0) v = fe_mul(pow_blocks(x4096, blockIdx.x), xshift);  // x^(jb + shift)
-  T[tid] = v;
+  RFr v = rx_unpack(x16);
+  if (tid == 0) v = rx_mul(pow_blocks_rx(rx_unpack(x4096), blockIdx.x), rx_unpack(xshift));
+  T[tid] = rx_pack(v);
   __syncthreads();
   for (uint32_t h = 1; h < 256; h <<= 1) {  // inclusive product scan
-    const Fr o = tid >= h ? T[tid - h] : fe_one<FrCfg>();
+    const RFr o = tid >= h ? rx_unpack(T[tid - h]) : rx_one<FrCfg>();
     __syncthreads();
-    if (tid >= h) T[tid] = fe_mul(T[tid], o);
+    if (tid >= h) T[tid] = rx_pack(rx_mul(rx_unpack(T[tid]), o));
     __syncthreads();
   }
   const uint64_t j0 = jb + (uint64_t)tid * 16;
   if (j0 >= len) return;
-  Fr pw = T[tid];
+  RFr pw = rx_unpack(T[tid]);
+  const RFr xr = rx_unpack(x);
   const uint64_t j1 = j0 + 16 < len ? j0 + 16 : len;
   for (uint64_t j = j0; j < j1; ++j) {
-    stf(&y[j], fe_mul(ldf(&c[j]), pw));
-    pw = fe_mul(pw, x);
+    stf(&y[j], rx_pack_canonical(rx_mul(ldr(&c[j]), pw)));
+    pw = rx_mul(pw, xr);
   }
 }
 
@@ -614,7 +617,8 @@ int pk_scale_powers(const Fr* c, uint64_t len, const Fr& x, uint64_t shift, Fr* 
   for (int i = 0; i < 8; ++i) x4096 = fe_sqr(x4096);
   const Fr xshift = fe_pow_u64(x, shift);
   hipLaunchKernelGGL(k_scale_powers, dim3(blocks_for((len + 15) / 16, 256)), dim3(256), 0, s, c, len,
-                     x, x16, x4096, xshift, y);
+                     fe_to_rx_domain(x), fe_to_rx_domain(x16), fe_to_rx_domain(x4096),
+                     fe_to_rx_domain(xshift), y);
   PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
 }

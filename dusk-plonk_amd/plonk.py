@@ -40,7 +40,8 @@ ABI_SYMBOLS = (
     "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
     "plk_srs_last_msm_stats", "plk_debug_field_op", "plk_commit_batch_dev",
-    "plk_srs_setup_range", "plk_g1_sum", "plk_srs_msm_stats_reset", "plk_srs_cum_msm_stats",
+    "plk_srs_setup_range", "plk_g1_sum", "plk_msm_sharded", "plk_srs_msm_stats_reset",
+    "plk_srs_cum_msm_stats",
     # prover (dusk-plonk_amd/prover.py binds these)
     "plk_composer_create", "plk_composer_destroy", "plk_composer_size",
     "plk_composer_append_witness", "plk_composer_witness_value", "plk_composer_set_witness",
@@ -109,6 +110,7 @@ def _lib():
             "plk_commit_batch_dev": (i32, [vp, vp, vp, sz, vp, vp, vp]),
             "plk_srs_setup_range": (i32, [vp, vp, u64, sz, vp, pp]),
             "plk_g1_sum": (i32, [vp, sz, vp]),
+            "plk_msm_sharded": (i32, [vp, i32, vp, sz, vp]),
             "plk_srs_msm_stats_reset": (i32, [vp]),
             "plk_srs_cum_msm_stats": (i32, [vp, C.POINTER(C.c_double), C.POINTER(u64),
                                             C.POINTER(u64), C.POINTER(u64)]),
@@ -326,6 +328,17 @@ def g1_sum(points: np.ndarray) -> Commitment:
     pts = np.ascontiguousarray(np.asarray(points, dtype=np.uint64).reshape(-1, 13))
     out = np.zeros(13, dtype=np.uint64)
     _check(_lib().plk_g1_sum(_ptr(pts), pts.shape[0], _ptr(out)), "plk_g1_sum")
+    return Commitment(out)
+
+
+def msm_sharded(shards, scalars) -> Commitment:
+    """One MSM over consecutive SRS slices held by different GPUs of this process
+    (PlonkParams.setup_range per device, in order): plk_msm_sharded."""
+    vals = _as_fr_array(scalars)
+    hs = (C.c_void_p * len(shards))(*[s._h.value for s in shards])
+    out = np.zeros(13, dtype=np.uint64)
+    _check(_lib().plk_msm_sharded(hs, len(shards), _ptr(vals), vals.shape[0], _ptr(out)),
+           "plk_msm_sharded")
     return Commitment(out)
 
 

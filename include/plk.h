@@ -136,6 +136,16 @@ int plk_commit_batch_dev(plk_srs* srs, const plk_fr* const* d_coeffs, const size
  * all-gather of per-GPU partial commitments of a sharded MSM. Needs no GPU. */
 int plk_g1_sum(const plk_g1* points, size_t n, plk_g1* out);
 
+/* One large MSM split over the GPUs of a node from ONE process:
+ * per_gpu[i] holds the SRS points following those of per_gpu[0..i-1] (e.g.
+ * plk_srs_setup_range on consecutive ranges, one slice per device). Each slice's MSM of its
+ * scalar slice runs concurrently (one host thread per slice, each on its own device and
+ * stream) and the partial points are folded on the host (plk_g1_sum):
+ * out = sum_{i<len} scalars[i] * g1[i], len <= total points. The multi-process form (one
+ * rank per GPU, RCCL all-gather of the partials) is dusk-plonk_amd/parallel.py. */
+int plk_msm_sharded(plk_srs* const* per_gpu, int n_gpu, const plk_fr* scalars, size_t len,
+                    plk_g1* out);
+
 /* ---- instrumentation (bench / profiling) ------------------------------------------- */
 /* Milliseconds of the dominant kernel of the most recent plk_commit/plk_msm on this SRS
  * (bucket accumulation), measured with HIP events on the launching stream; and the

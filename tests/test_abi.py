@@ -38,6 +38,7 @@ def test_null_arguments_are_rejected_without_gpu(plk):
     assert lib.plk_ntt(None, None, 0, 1, 0) == plk.PLK_E_ARG
     assert lib.plk_commit(None, None, 0, None) == plk.PLK_E_ARG
     assert lib.plk_srs_len(None, None) == plk.PLK_E_ARG
+    assert lib.plk_msm_sharded(None, 0, None, 0, None) == plk.PLK_E_ARG
 
 
 def test_device_count_never_fails(plk):

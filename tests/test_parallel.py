@@ -140,3 +140,21 @@ def _gpu_worker(rank, world, port, q):
 def test_sharded_commit_two_ranks_one_gpu(plk, gpu_ctx):
     out = _spawn(_gpu_worker, 2)
     assert out == {0: True, 1: True}
+
+
+@pytest.mark.gpu
+def test_msm_sharded_single_process(plk, gpu_ctx):
+    """plk_msm_sharded: one process, consecutive SRS slices (PlonkParams.setup_range; here
+    all on the one visible device), even and uneven cuts, full and partial scalar lengths,
+    against the unsharded MSM."""
+    from oracle_lib import random_fr
+    from dusk_plonk_amd.plonk import msm_sharded
+    n = 1 << 12
+    tau = random_fr(1, seed=41)[0]
+    full = plk.PlonkParams.setup(12, tau, gpu_ctx, n_points=n)
+    sc = random_fr(n, seed=42)
+    for cuts in ([0, n // 2, n], [0, 1000, 1001, n]):
+        shards = [plk.PlonkParams.setup_range(tau, lo, hi - lo, gpu_ctx)
+                  for lo, hi in zip(cuts, cuts[1:])]
+        for m in (n, 1500, 1000, 1):
+            assert np.array_equal(msm_sharded(shards, sc[:m]).words, full.msm(sc[:m]).words), (cuts, m)
