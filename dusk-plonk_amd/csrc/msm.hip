@@ -5,7 +5,7 @@
 //
 // Design (fixed-base Pippenger, all windows folded into one bucket set):
 //  * SRS load (srs.hip): table[w][i] = 2^(c*w) * P_i in affine form, w < W, resident in
-//    HBM (W * n * 96 B: 1.5 GB at n = 2^20, c = 17, W = 15). Commit bases are always an
+//    HBM (W * n * 96 B: 1.6 GB at n = 2^20, c = 16, W = 16). Commit bases are always an
 //    SRS prefix, so the table is built once.
 //  * Per MSM: each scalar s is first brought to [0, (r-1)/2] (s or r - s with the signs
 //    flipped, scalar_half), then recoded into W = ceil(255/c) signed c-bit digits
