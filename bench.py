@@ -62,9 +62,11 @@ def parse():
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4); "
                          "0 = min(32, 2 x lanes): more lanes than queues serialise on them")
-    ap.add_argument("--mode", choices=["prove", "hotpath"], default="prove",
+    ap.add_argument("--mode", choices=["prove", "hotpath", "ntt", "msm"], default="prove",
                     help="prove: full Prover::create_proof (synthesis + 5 rounds + openings); "
-                         "hotpath: only the 19 NTTs + 11 MSMs of one proof")
+                         "hotpath: only the 19 NTTs + 11 MSMs of one proof; ntt / msm: "
+                         "BASELINE.json configs[1] / configs[2], the standalone 2^k dft+idft "
+                         "pair or G1 MSM, bit-exact against the oracle after the timed loop")
     ap.add_argument("--shard-msm", action="store_true",
                     help="one proof per step; every commit sharded over the ranks (RCCL "
                          "all-gather of partial points + host fold); NTTs replicated")
@@ -322,17 +324,22 @@ def valu_roofline(adds_per_s):
             "mads_per_point_add": MADS_PER_MIXED_ADD}
 
 
-def load_pmc_traffic(kernel_substr: str, key: str = "hbm_bytes_per_launch"):
+def load_pmc_traffic(kernel_substr: str, key: str = "hbm_bytes_per_launch",
+                     fname: str = "pmc_traffic.json"):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, made by tools/gpu_pmc.sh + tools/pmc_summary.py from the
-    default bench command). key "hbm_bytes_last_launch" = the run's last dispatch."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
+    default bench command). key "hbm_bytes_last_launch" = the run's last dispatch. A summary
+    with a "units" field (tools/gpu_configs.sh: the transforms or MSMs its run performed)
+    gives bytes per unit instead: all launches of the kernel / units."""
+    f = ROOT / "profiles" / fname
     if not f.exists():
         return None
     try:
         d = json.loads(f.read_text())
         for name, rec in d.get("kernels", {}).items():
             if kernel_substr in name:
+                if "units" in d:
+                    return rec["hbm_bytes_per_launch"] * rec["launches"] / d["units"]
                 return rec.get(key, rec.get("hbm_bytes_per_launch"))
     except Exception:
         return None
@@ -453,6 +460,137 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
         dist.destroy_process_group()
 
 
+def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
+    """BASELINE.json configs[1] (standalone 2^k BlsScalar NTT/iNTT) and configs[2]
+    (standalone 2^k G1 MSM on SRS bases) on one GPU per rank, replicas only (each rank its
+    own transform / MSM). Inputs are resident in HBM; one step = dft + idft (ntt) or one
+    MSM (msm). After the timed loop the result is checked bit-exact against the oracle
+    (tests/oracle_lib.py), whose timing on the same input is the cpu_baseline."""
+    s = torch.cuda.current_stream().cuda_stream
+    ctx = plk.Context.default(device.index or 0)
+    x = rand_fr_dev(torch, n, 4242 + rank, device)
+    ev = []
+    if args.mode == "ntt":
+        fft = plk.Fft(k, ctx)
+        y, z = torch.empty_like(x), torch.empty_like(x)
+
+        def step(timed):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
+            if timed:
+                e[0].record()
+            fft.ntt_dev(x.data_ptr(), y.data_ptr(), n, 1, False, s)
+            if timed:
+                e[1].record()
+            fft.ntt_dev(y.data_ptr(), z.data_ptr(), n, -1, False, s)
+            if timed:
+                e[2].record()
+                ev.append(e)
+        units = 2 * n
+    else:
+        tau = np.asarray(np.random.default_rng(0x5EED).integers(1, 2**62, 4), dtype=np.uint64)
+        tau[3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+        pp = plk.PlonkParams.setup(k, tau, ctx)
+        coms = []
+
+        def step(timed):
+            coms.append(pp.commit_dev(x.data_ptr(), n, s))  # returns the affine point
+            if timed:
+                ev.append(pp.last_msm_stats())
+        units = n
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    ev.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps = args.steps
+    if args.mode == "ntt":
+        t_dft = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+        t_idft = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
+        launch_ms = (t_dft + t_idft) / 2
+        alg_bytes = 64.0 * n  # SURVEY §8d: one read + one write of 32 B per point
+        roof = {"bound": "hbm", "kernel": "k_ntt_pass (all passes of one transform)",
+                "achieved": alg_bytes / (launch_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "traffic": load_pmc_traffic("k_ntt_pass", fname=f"pmc_traffic_ntt{k}.json"),
+                "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": launch_ms,
+                "dft_ms": t_dft, "idft_ms": t_idft,
+                "note": "per transform (all its Stockham passes; traffic summed over them); "
+                        "instruction-bound, see DESIGN §3"}
+        metric = f"standalone BlsScalar dft+idft points/s at n=2^{k} (BASELINE configs[1])"
+        workload = f"Fft::dft + Fft::idft of one 2^{k}-point Fr vector, device-resident"
+    else:
+        launch_ms = sum(e[0] for e in ev) / steps
+        adds = sum(e[1] for e in ev) / steps
+        alg_bytes = 128.0 * n  # SURVEY §8d: N * (32 B scalar + 96 B base)
+        roof = {"bound": "hbm", "kernel": "k_accumulate", "achieved":
+                alg_bytes / (launch_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "traffic": load_pmc_traffic("k_accumulate", fname=f"pmc_traffic_msm{k}.json"),
+                "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": launch_ms,
+                "point_adds_per_launch": adds, "point_adds_per_s": adds / (launch_ms * 1e-3),
+                "valu": valu_roofline(adds / (launch_ms * 1e-3)),
+                "note": "integer-VALU-bound (no MFMA); HBM is the secondary roofline"}
+        metric = f"standalone G1 MSM points/s at n=2^{k} (BASELINE configs[2])"
+        workload = f"KZG10 commit: one 2^{k}-point G1 MSM, random Fr scalars, SRS bases"
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    result = {
+        "metric": metric, "value": units * steps * world / elapsed, "unit": "points/s",
+        "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32-limb Montgomery Fr/Fp (integer)",
+        "data": "synthetic (uniform Fr)",
+        "config": {"workload": workload, "n": n, "log_n": k,
+                   "parallelism": f"replicas x{world}"},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_lib
+        orc = oracle_lib.load()
+        xh = x.cpu().numpy().view(np.uint64)
+        if args.mode == "ntt":
+            t0 = time.perf_counter()
+            want = orc.dft(xh, k, threads)
+            t1 = time.perf_counter()
+            back = orc.idft(want, k, threads)
+            t2 = time.perf_counter()
+            exact = (np.array_equal(y.cpu().numpy().view(np.uint64), want)
+                     and np.array_equal(z.cpu().numpy().view(np.uint64), back)
+                     and np.array_equal(back, xh))
+            cpu_s = t2 - t0
+            sample = (f"oracle/plk_oracle.c orc_ntt (OpenMP {threads} threads): dft(2^{k}) "
+                      f"{t1 - t0:.3f}s + idft(2^{k}) {t2 - t1:.3f}s on the same input")
+        else:
+            t0 = time.perf_counter()
+            want = orc.msm(pp.points(0, n), xh, threads)
+            cpu_s = time.perf_counter() - t0
+            exact = all(np.array_equal(c.words, want) for c in coms)
+            sample = (f"oracle/plk_oracle.c orc_msm (Pippenger, OpenMP {threads} threads): "
+                      f"one MSM(2^{k}) on the same SRS and scalars {cpu_s:.2f}s")
+        result["bit_exact_vs_oracle"] = bool(exact)
+        result["cpu_baseline"] = {"value": units / cpu_s, "unit": "points/s", "cores": threads,
+                                  "kind": "port", "host": host_info(), "sample": sample}
+        if not exact:
+            print(json.dumps(result), flush=True)
+            raise SystemExit("GPU result differs from the oracle")
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.lanes <= 0:
@@ -484,6 +622,8 @@ def main():
     # context's own stream, so events recorded by torch would not bracket our kernels.
     stream = torch.cuda.Stream(device=device)
     torch.cuda.set_stream(stream)
+    if args.mode in ("ntt", "msm"):
+        return run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n)
     shard = args.shard_msm and world > 1
     if args.mode == "prove" and not shard:
         return run_full(args, plk, torch, dist, world, rank, device, k, n)
