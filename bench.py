@@ -67,6 +67,9 @@ def parse():
                          "hotpath: only the 19 NTTs + 11 MSMs of one proof; ntt / msm: "
                          "BASELINE.json configs[1] / configs[2], the standalone 2^k dft+idft "
                          "pair or G1 MSM, bit-exact against the oracle after the timed loop")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group for the barrier / max-over-ranks timing (nccl = RCCL); "
+                         "gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--shard-msm", action="store_true",
                     help="one proof per step; every commit sharded over the ranks (RCCL "
                          "all-gather of partial points + host fold); NTTs replicated")
@@ -94,7 +97,8 @@ class HotPath:
         if shard:  # this rank's slice of the 2^k + 8 powers
             from dusk_plonk_amd.parallel import ShardedPlonkParams
             self.pp = ShardedPlonkParams(k, tau, ctx=self.ctx)
-            self.device = device
+            # partials all-gathered from HBM over RCCL; from host memory under gloo
+            self.device = device if torch.distributed.get_backend() == "nccl" else None
         else:
             self.pp = plk.PlonkParams.setup(k, tau, self.ctx)  # 2^k + 8 powers
         r = lambda s: rand_fr_dev(torch, n, seed + s, device)  # noqa: E731
@@ -346,6 +350,14 @@ def load_pmc_traffic(kernel_substr: str, key: str = "hbm_bytes_per_launch",
     return None
 
 
+def max_over_ranks(torch, dist, elapsed: float, device) -> float:
+    """The slowest rank's time (all_reduce MAX; a host tensor under gloo)."""
+    on = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def run_full(args, plk, torch, dist, world, rank, device, k, n):
     # `lanes` independent provers per GPU (own context / stream, SRS, key, scratch and
     # synthesis thread), each driven by its own host thread: a proof server keeps several
@@ -380,9 +392,7 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(torch, dist, elapsed, device)
     steps = args.steps
     # roofline: k_accumulate over every launch of the timed region (HIP events on each
     # lane's stream; with several lanes the kernels share the GPU, as in the workload)
@@ -512,9 +522,7 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(torch, dist, elapsed, device)
     steps = args.steps
     if args.mode == "ntt":
         t_dft = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
@@ -608,8 +616,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one rank per GPU; ranks beyond the device count share GPUs (a gloo rehearsal of
+        # the multi-rank path on a one-GPU box: RCCL refuses two ranks on one device)
+        local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     device = torch.device("cuda", torch.cuda.current_device())
@@ -643,9 +657,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(torch, dist, elapsed, device)
 
     ntt_n = [a.elapsed_time(b) for a, b in hp.ntt_ms["n"]]
     ntt_8n = [a.elapsed_time(b) for a, b in hp.ntt_ms["8n"]]
