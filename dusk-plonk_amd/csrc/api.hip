@@ -443,16 +443,22 @@ int plk_msm_sharded(plk_srs* const* per_gpu, int n_gpu, const plk_fr* scalars, s
   std::vector<plk_g1> part((size_t)n_gpu, plk_g1{});
   std::vector<int> status((size_t)n_gpu, PLK_OK);
   std::vector<std::thread> workers;
+  workers.reserve((size_t)n_gpu);
   size_t off = 0;
-  for (int i = 0; i < n_gpu; ++i) {
-    plk_srs* s = per_gpu[i];
-    const size_t cnt = off < len ? std::min(s->n, len - off) : 0;
-    part[i].infinity = 1;
-    if (cnt)
-      workers.emplace_back([&part, &status, s, i, cnt, p = scalars + off]() {
-        status[i] = plk_msm(s, p, cnt, &part[i]);
-      });
-    off += s->n;
+  try {
+    for (int i = 0; i < n_gpu; ++i) {
+      plk_srs* s = per_gpu[i];
+      const size_t cnt = off < len ? std::min(s->n, len - off) : 0;
+      part[i].infinity = 1;
+      if (cnt)
+        workers.emplace_back([&part, &status, s, i, cnt, p = scalars + off]() {
+          status[i] = plk_msm(s, p, cnt, &part[i]);
+        });
+      off += s->n;
+    }
+  } catch (...) {  // a thread that failed to start: drain the started ones, then report
+    for (auto& t : workers) t.join();
+    throw;
   }
   for (auto& t : workers) t.join();
   for (int i = 0; i < n_gpu; ++i)
