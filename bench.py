@@ -1,25 +1,25 @@
 #!/usr/bin/env python3
-"""bench.py — PLONK prover hot path on MI355X (BLS12-381), the BASELINE.json metric.
+"""bench.py — the BASELINE.json metric: PLONK prover constraints/s (BLS12-381) on MI355X.
 
-A step = the hot path of ONE `Prover::create_proof` at n = 2^k (default k = 20), in the
-reference's order and with the reference's data flow:
+Default step (mode "prove"): every prover lane of every rank completes ONE full
+`Prover::create_proof` (src/prover.rs:67-474) at n = 2^k (default k = 20) on the synthetic
+arithmetic-chain circuit of SURVEY §8d item 4 plus one public input: host synthesis of a fresh
+witness (C++ composer, overlapped with the previous proof) + the five rounds + both openings
+on the GPU, proof back on the host. The key (PlonkKey::compile) and the SRS are built once per
+GPU outside the timed region and shared by the GPU's lanes (plk_prover). Per proof the GPU
+runs 13 transforms (6 idft(n): 4 wires, z, PI; 6 coset_dft(8n): z, 4 wires, PI; 1
+coset_idft(8n)) and 11 MSMs; the reference's other 6 transforms are per-key constants here
+(4 sigma dft(n): the key holds their Lagrange values; L1's idft(n) + coset_dft(8n)).
 
-  round 1   4x idft(n) wires          -> 4x commit            (prover.rs:121-136)
-  round 2   4x dft(n) sigmas (permutation.rs:232), idft(n) z -> commit (prover.rs:192-194)
-  round 3   idft(n) PI, idft(n) L1 (quotient_poly.rs:271), 7x coset_dft(8n)
-            (quotient_poly.rs:54-58,145,237), coset_idft(8n) (:115) -> 4x commit of the
-            t chunks (prover.rs:262-265)
-  openings  2x commit (prover.rs:440,452)
-
-= 19 NTTs + 11 MSMs, inputs synthetic and resident in HBM, each commitment copied to the
-host (the transcript needs it) exactly where the reference blocks on it. NOT in the step:
-the quotient/grand-product elementwise loops, blinding, Horner evaluations and the
-aggregate-witness divisions (SURVEY §8f rows 1-3, next rounds); their HBM/VALU cost is
-small next to the 30 transforms but the value is labelled `hot_path_only`.
-
-value = constraints/s = n * steps * world_size / max-over-ranks time. Multi-GPU: one
-proof per rank per step (proof batches shard across GPUs, no data-path collective:
-scaling "weak"); torch.distributed only for the barrier and the max-time reduction.
+value = constraints/s = n * proofs / max-over-ranks time.
+  * default: proof batches — every rank proves its own proofs (weak scaling, no
+    data-path collective; torch.distributed only for the barrier and the max reduction);
+  * --shard-msm (BASELINE configs[4]): every rank proves the SAME proofs and each commit is
+    split over the ranks by SRS slice (plk_prover_shard: one RCCL all-gather of partial
+    points per commit group, host fold) — strong scaling of proof latency.
+`--gpus N` without a launcher starts N ranks itself (torch.distributed.run, 127.0.0.1).
+Other modes: hotpath (only the NTT/MSM calls of one proof), ntt / msm (BASELINE configs[1] /
+[2], checked bit-exact against the oracle after the timed loop).
 """
 from __future__ import annotations
 
@@ -47,12 +47,17 @@ MADS_PER_MIXED_ADD = 8 * 196 + 2 * 105 + 9 * 196
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU). Without WORLD_SIZE in the environment and N > 1, "
+                         "bench.py launches N ranks itself (torch.distributed.run); under a "
+                         "launcher N must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads; 0 = OMP_NUM_THREADS if set (the GPU box's CPU "
+                         "share per GPU), else every core in this process's affinity mask")
     ap.add_argument("--lanes", type=int, default=0,
                     help="concurrent prover lanes per GPU (prove mode): independent contexts "
                          "with their own streams, each driven by a host thread. 0 = 8 at "
@@ -71,8 +76,9 @@ def parse():
                     help="process group for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--shard-msm", action="store_true",
-                    help="one proof per step; every commit sharded over the ranks (RCCL "
-                         "all-gather of partial points + host fold); NTTs replicated")
+                    help="BASELINE configs[4]: all ranks prove the same proofs, every commit "
+                         "split over the ranks by SRS slice (RCCL all-gather of partial points "
+                         "+ host fold); NTT / elementwise rounds replicated")
     return ap.parse_args()
 
 
@@ -162,36 +168,60 @@ class HotPath:
         return coms
 
 
-class FullProver:
-    """One step = Prover::create_proof on an n = 2^k synthetic arithmetic-chain circuit
-    (m = n - 8 gates incl. the composer's 6 initial gates): synthesis of a fresh witness
-    (C++ composer) + all five rounds + openings on the GPU, proof bytes back on the host.
-    The key (PlonkKey::compile) and the SRS are built once, outside the timed region."""
+BENCH_TAU_SEED = 0x5EED
 
-    def __init__(self, plk, k: int, seed: int, ctx=None):
+
+def bench_tau():
+    tau = np.asarray(np.random.default_rng(BENCH_TAU_SEED).integers(1, 2**62, 4), dtype=np.uint64)
+    tau[3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+    return tau
+
+
+def bench_circuit(Plonk, chain_gates: int, seed: int):
+    """The bench circuit: Plonk::initialize (6 gates), `chain_gates` chained gates
+    x' = x*y + x (fresh SplitMix64 witness from `seed`) and one public input (lib.rs:708-719),
+    so the per-proof PI transforms the reference runs (prover.rs:229, quotient_poly.rs:145)
+    are in the step."""
+    cs = Plonk()
+    cs.synthetic_chain(chain_gates, seed)
+    cs.append_public((seed * 0x9E3779B97F4A7C15 + 12345) % (1 << 250))
+    return cs
+
+
+class ProverBase:
+    """Per GPU, built once outside the timed region: the SRS (2^k + 8 powers, window table
+    in HBM) and the compiled proving key, shared by all of this GPU's prover lanes."""
+
+    def __init__(self, plk, k: int, ctx):
         from dusk_plonk_amd.prover import PlonkKey, Plonk
-        self.plk, self.k, self.n = plk, k, 1 << k
+        self.plk, self.k, self.n, self.ctx = plk, k, 1 << k, ctx
         self.Plonk = Plonk
-        self.gates = self.n - 8 - 6
-        tau = np.asarray(np.random.default_rng(0x5EED).integers(1, 2**62, 4), dtype=np.uint64)
-        tau[3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
-        self.pp = plk.PlonkParams.setup(k, tau, ctx=ctx)
-        cs = Plonk()
-        cs.synthetic_chain(self.gates, seed)
-        self.prover, self.vd = PlonkKey.compile_composer(self.pp, b"bench", cs)
-        self.seed = seed
-        self.synth_s = []
-        self.prove_s = []
-        # synthesis of proof k+1 (host C++ composer, GIL released in ctypes) overlaps the
-        # GPU proving of proof k, as in a proof server; both are inside the timed loop
+        self.chain = self.n - 8 - 6 - 1  # m = n - 8 gates: 6 initial + chain + 1 public
+        self.tau = bench_tau()
+        self.pp = plk.PlonkParams.setup(k, self.tau, ctx=ctx)
+        self.prover, self.vd = PlonkKey.compile_composer(
+            self.pp, b"bench", bench_circuit(Plonk, self.chain, 1))
+        self.gates = self.prover.m
+
+
+class ProofLane:
+    """One concurrent prover (plk_prover over the shared key: own stream, MSM workspace and
+    scratch) with its own synthesis thread: synthesis of proof k+1 (host C++ composer, GIL
+    released in ctypes) overlaps the GPU proving of proof k, as in a proof server; both are
+    inside the timed loop."""
+
+    def __init__(self, base: ProverBase, seed: int):
         import concurrent.futures as cf
+        self.base = base
+        self.lane = base.prover.lane()
+        self.seed = seed
+        self.synth_s, self.prove_s = [], []
         self.pool = cf.ThreadPoolExecutor(1)
         self.next = self.pool.submit(self._synth, self.seed + 1)
 
     def _synth(self, seed):
         t0 = time.perf_counter()
-        cs = self.Plonk()
-        cs.synthetic_chain(self.gates, seed)  # a fresh witness every proof
+        cs = bench_circuit(self.base.Plonk, self.base.chain, seed)  # a fresh witness
         return cs, time.perf_counter() - t0
 
     def step(self, timed=False):
@@ -199,7 +229,7 @@ class FullProver:
         cs, ts = self.next.result()
         self.next = self.pool.submit(self._synth, self.seed + 1)
         t1 = time.perf_counter()
-        proof, pi = self.prover.prove_composer(cs, self.seed)
+        proof, pi = self.lane.prove_composer(cs, self.seed)
         t2 = time.perf_counter()
         if timed:
             self.synth_s.append(ts)
@@ -251,8 +281,7 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
     orc = oracle_lib.load()
     ks = min(k, k_sample)
     n, ns = 1 << k, 1 << ks
-    cs = Plonk()
-    cs.synthetic_chain(ns - 14, 77)
+    cs = bench_circuit(Plonk, ns - 15, 77)
     gates, wit = cs.export()
     trim = (1 << (gates.shape[0] + 6 - 1).bit_length()) + 8
     res = orc.prove(gates, wit, pp.points(0, trim), b"cpu-baseline", 5, threads)
@@ -279,15 +308,29 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
         per_proof = 11 * t_msm + 11 * t_ntt + 8 * t_ntt8 + other_s * (n / ns)
     # the same restated prover on ONE core, at 2^12 (seconds, not extrapolated)
     k1 = min(k, 12)
-    cs1 = Plonk()
-    cs1.synthetic_chain((1 << k1) - 14, 78)
+    cs1 = bench_circuit(Plonk, (1 << k1) - 15, 78)
     g1, w1 = cs1.export()
     trim1 = (1 << (g1.shape[0] + 6 - 1).bit_length()) + 8
     r1 = orc.prove(g1, w1, pp.points(0, trim1), b"cpu-baseline-1", 5, 1)
     one_core_s = float(r1["timing_ns"][6]) / 1e9  # create_proof phase (compile excluded)
+    hi = host_info()
     return {
         "value": n / per_proof, "unit": "constraints/s", "cores": threads, "kind": "port",
-        "host": host_info(),
+        "host": hi,
+        "extrapolated": ks != k,
+        "measure": "latency of ONE proof on `cores` threads (the GPU value is the throughput of "
+                   "all its lanes' proofs in flight)",
+        "all_cores_projection": {
+            "cores": hi["usable_cores"],
+            "value": n / per_proof * (hi["usable_cores"] or threads) / threads,
+            "note": "upper bound: the measured rate scaled linearly to every core in the "
+                    "affinity mask (perfect scaling assumed; the GPU box allots "
+                    f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')} per GPU)"},
+        "node_throughput_upper_bound": {
+            "value": (hi["usable_cores"] or threads) * (1 << k1) / one_core_s,
+            "note": f"usable cores x the single-core rate at 2^{k1} (independent proofs, one per "
+                    "core; per-constraint cost grows with n, so this bounds the node's 2^"
+                    f"{k} throughput from above)"},
         "single_core": {"n": 1 << k1, "seconds": one_core_s,
                         "value": (1 << k1) / one_core_s, "unit": "constraints/s",
                         "note": "full create_proof (key compile excluded) on 1 thread"},
@@ -358,31 +401,64 @@ def max_over_ranks(torch, dist, elapsed: float, device) -> float:
     return float(t.item())
 
 
-def run_full(args, plk, torch, dist, world, rank, device, k, n):
-    # `lanes` independent provers per GPU (own context / stream, SRS, key, scratch and
-    # synthesis thread), each driven by its own host thread: a proof server keeps several
-    # proofs in flight so one proof's host phases and reduction tails overlap another's
-    # kernels. One step = every lane completes one proof.
+def cpu_threads(args) -> int:
+    """CPU baseline threads: --cpu-threads, else OMP_NUM_THREADS (set on the GPU box to the
+    CPU share of one GPU), else every core in this process's affinity mask."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return host_info()["usable_cores"] or 1
+
+
+def acc_roofline(ms_total, launches, adds, points, label):
+    """k_accumulate: algorithmic bytes (128 B per MSM point) and mixed additions
+    per launch over the average launch duration (dispatch-stamped events)."""
+    ms = ms_total / launches
+    alg = 128.0 * points / launches
+    return {"avg_launch_ms": ms, "launches": launches,
+            "algorithmic_bytes_per_launch": alg,
+            "achieved_gbs": alg / (ms * 1e-3) / 1e9,
+            "point_adds_per_launch": adds / launches,
+            "point_adds_per_s": adds / (ms_total * 1e-3),
+            "valu": valu_roofline(adds / (ms_total * 1e-3)), "timing": label}
+
+
+def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
+    # `lanes` concurrent provers per GPU over ONE shared key and SRS (plk_prover: own
+    # stream, MSM workspace, scratch), each driven by its own host thread: a proof server
+    # keeps several proofs in flight so one proof's host phases and reduction tails overlap
+    # another's kernels. One step = every lane completes one proof.
     L = max(1, args.lanes)
-    dev = torch.cuda.current_device()  # this rank's GPU (LOCAL_RANK under torchrun)
-    lanes = [FullProver(plk, k, seed=1000 * rank + 17 + 101 * l,
-                        ctx=plk.Context.default(dev) if l == 0 else plk.Context(dev))
-             for l in range(L)]
-    fp = lanes[0]
+    ctx = plk.Context.default(torch.cuda.current_device())
+    base = ProverBase(plk, k, ctx)
+    # sharded: every rank proves the same proofs (same seeds), commits split by SRS slice
+    lane_seed = (lambda l: 17 + 101 * l) if shard else (lambda l: 1000 * rank + 17 + 101 * l)
+    lanes = [ProofLane(base, lane_seed(l)) for l in range(L)]
+    if shard:
+        from dusk_plonk_amd.parallel import shard_prover_lane, srs_slice
+        comm_dev = device if dist.get_backend() == "nccl" else None
+        sl = srs_slice(base.tau, base.pp.n, world, rank, ctx)  # one slice per GPU, all lanes
+        # one process group per lane: a lane's exchanges are ordered within its own group,
+        # lanes run concurrently (every rank creates the groups in the same order)
+        groups = [dist.new_group(backend=dist.get_backend()) for _ in range(L)]
+        for ln, g in zip(lanes, groups):
+            shard_prover_lane(ln.lane, base.tau, base.pp.n, g, comm_dev, ctx, slice_=sl)
     import concurrent.futures as cf
     drivers = cf.ThreadPoolExecutor(L)
 
-    def run(count, timed):
+    def run(count, timed, which=None):
         def one(lane):
             for _ in range(count):
                 lane.step(timed=timed)
-        for f in [drivers.submit(one, lane) for lane in lanes]:
+        for f in [drivers.submit(one, ln) for ln in (which or lanes)]:
             f.result()
 
     run(args.warmup, False)
     torch.cuda.synchronize()
-    for lane in lanes:
-        lane.pp.msm_stats_reset()
+    for ln in lanes:
+        ln.lane.msm_stats(reset=True)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -394,78 +470,88 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n):
     if world > 1:
         elapsed = max_over_ranks(torch, dist, elapsed, device)
     steps = args.steps
-    # roofline: k_accumulate over every launch of the timed region (HIP events on each
-    # lane's stream; with several lanes the kernels share the GPU, as in the workload)
+    # k_accumulate inside the workload (all lanes' launches; they share the chip) ...
     acc_ms = launches = adds = points = 0
-    for lane in lanes:
-        m_, l_, a_, p_ = lane.pp.cum_msm_stats()
+    for ln in lanes:
+        m_, l_, a_, p_ = ln.lane.msm_stats(reset=True)
         acc_ms, launches, adds, points = acc_ms + m_, launches + l_, adds + a_, points + p_
-    cbits = fp.pp.last_msm_stats()[2]
-    # the same kernel with the GPU to itself: one more proof on lane 0 after the timed
-    # region (the in-workload figure above shares the chip with the other lanes' kernels)
-    solo = None
-    if L > 1:
-        fp.pp.msm_stats_reset()
-        fp.step(timed=False)
-        torch.cuda.synchronize()
-        s_ms, s_l, s_a, s_p = fp.pp.cum_msm_stats()
-        if s_l and s_ms > 0:
-            solo = {"avg_launch_ms": s_ms / s_l, "launches": s_l,
-                    "point_adds_per_s": s_a / (s_ms * 1e-3),
-                    "valu": valu_roofline(s_a / (s_ms * 1e-3)),
-                    "note": "one proof with no other lane running (outside the timed region)"}
+    # ... and with the GPU to itself: one more proof on lane 0 after the timed region. The
+    # solo durations are the kernel's own (the in-workload ones overlap other lanes' kernels)
+    run(1, False, [lanes[0]])
+    torch.cuda.synchronize()
+    s_ms, s_l, s_a, s_p = lanes[0].lane.msm_stats(reset=True)
+    cbits = base.pp.last_msm_stats()[2]
+    proofs = L if shard else L * world
+    transforms = "13 transforms (6 idft(n), 6 coset_dft(8n), 1 coset_idft(8n)) + 11 MSMs"
     result = {
         "metric": "PLONK prover constraints/sec (BLS12-381) at n=2^16 and 2^20, 1/2/4/8 GPUs",
-        "value": n * steps * L * world / elapsed,
+        "value": n * steps * proofs / elapsed,
         "unit": "constraints/s",
         "n_gpus": world,
         "steps": steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "u32-limb Montgomery Fr/Fp (integer)",
-        "data": "synthetic arithmetic-chain circuit x' = x*y + x, fresh SplitMix64 witness per proof",
+        "data": "synthetic arithmetic-chain circuit x' = x*y + x + 1 public input, fresh "
+                "SplitMix64 witness per proof",
         "config": {
-            "workload": f"full Prover::create_proof at n=2^{k} (m = {fp.gates + 6} gates): "
-                        "synthesis + 5 rounds + 2 openings, 19 NTTs + 11 MSMs on one GPU; "
-                        "host synthesis of the next proof overlaps the current GPU proof"
-                        + (f"; {L} proofs in flight per GPU (independent contexts/streams)"
-                           if L > 1 else ""),
-            "n": n, "log_n": k, "proofs_per_step": world * L,
-            "parallelism": f"proof-batch x{world * L} ({L} concurrent prover lane(s) per GPU)",
+            "workload": f"full Prover::create_proof at n=2^{k} (m = {base.gates} gates, 1 public "
+                        f"input): synthesis + 5 rounds + 2 openings = {transforms} per proof "
+                        "(the reference's 4 sigma dft(n) and L1's idft(n) + coset_dft(8n) are "
+                        "per-key constants here); host synthesis of the next proof overlaps "
+                        "the current GPU proof"
+                        + (f"; {L} proofs in flight per GPU (plk_prover lanes sharing one key "
+                           "and SRS)" if L > 1 else "")
+                        + (f"; every commit split over {world} GPUs by SRS slice (RCCL "
+                           "all-gather of partial points + host fold), NTT / elementwise "
+                           "rounds replicated on every GPU" if shard else ""),
+            "n": n, "log_n": k, "proofs_per_step": proofs,
+            "parallelism": (f"msm-shard x{world} x {L} lane(s)" if shard else
+                            f"proof-batch x{world * L} ({L} concurrent prover lane(s) per GPU)"),
             "msm_window_bits": cbits,
             "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
         },
         "breakdown_ms_per_step": {
-            "synthesis_host_overlapped": 1e3 * sum(sum(l.synth_s) for l in lanes) / (steps * L),
-            "prove_latency": 1e3 * sum(sum(l.prove_s) for l in lanes) / (steps * L),
+            "synthesis_host_overlapped": 1e3 * sum(sum(ln.synth_s) for ln in lanes) / (steps * L),
+            "prove_latency": 1e3 * sum(sum(ln.prove_s) for ln in lanes) / (steps * L),
         },
     }
-    # roofline of the dominant kernel (bucket accumulation of the last commit batch)
-    if launches and acc_ms > 0:
-        ms = acc_ms / launches
-        alg = 128.0 * points / launches  # N (32 + 96) bytes per MSM point
-        achieved = alg / (ms * 1e-3) / 1e9
+    # roofline of the dominant kernel (k_accumulate, ~60 % of a proof's GPU time) from its
+    # solo launches; the in-workload averages beside them
+    if s_l and s_ms > 0:
+        solo = acc_roofline(s_ms, s_l, s_a, s_p, "one proof with no other lane running, "
+                            "dispatch-stamped events (outside the timed region)")
+        inw = (acc_roofline(acc_ms, launches, adds, points, "all lanes inside the timed region; "
+                            "durations overlap other lanes' kernels (not the kernel's own time)")
+               if launches and acc_ms > 0 else None)
+        traffic = load_pmc_traffic("k_accumulate")
         result["roofline"] = {
-            "bound": "hbm", "kernel": "k_accumulate", "achieved": achieved, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": load_pmc_traffic("k_accumulate"),
-            "algorithmic_bytes_per_launch": alg, "avg_launch_ms": ms,
-            "launches": launches, "point_adds_per_launch": adds / launches,
-            "point_adds_per_s": adds / (acc_ms * 1e-3),
-            "valu": valu_roofline(adds / (acc_ms * 1e-3)),
-            "solo": solo,
-            "note": "integer-VALU-bound (no MFMA); HBM reported as the required secondary "
-                    "roofline; averages over the timed region's launches of all lanes "
+            "bound": "hbm", "kernel": "k_accumulate", "achieved": solo["achieved_gbs"],
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": solo["achieved_gbs"] / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "traffic_source": ("profiles/pmc_traffic.json (rocprofv3 PMC pass of the default bench "
+                               "command, stored; raw TCC FETCH+WRITE, FETCH not doubled)")
+            if traffic is not None else None,
+            "algorithmic_bytes_per_launch": solo["algorithmic_bytes_per_launch"],
+            "avg_launch_ms": solo["avg_launch_ms"], "launches": solo["launches"],
+            "point_adds_per_launch": solo["point_adds_per_launch"],
+            "point_adds_per_s": solo["point_adds_per_s"],
+            "valu": solo["valu"], "binding_roofline": "valu",
+            "solo": solo, "in_workload": inw,
+            "note": "integer-VALU-bound (no MFMA): the binding fraction is valu.frac "
+                    "(v_mad_u64_u32 issue); HBM reported as the required secondary roofline "
                     "(4 commit batches per proof: 4, 1, 4 and 2 MSMs)",
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline_full(k, fp.pp, threads)
+        result["cpu_baseline"] = cpu_baseline_full(k, base.pp, cpu_threads(args))
     if rank == 0:
         print(json.dumps(result), flush=True)
+    for ln in lanes:
+        ln.pool.shutdown(wait=True)
+        ln.lane.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -563,7 +649,7 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = cpu_threads(args)
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_lib
         orc = oracle_lib.load()
@@ -599,8 +685,28 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
         dist.destroy_process_group()
 
 
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N ranks of this same command under
+    torch.distributed.run (127.0.0.1) as a child process and return its exit code. Called
+    before anything touches the GPU (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus and args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus))
+    if world_env is not None and args.gpus is not None and args.gpus != int(world_env):
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
     if args.lanes <= 0:
         args.lanes = 8 if args.log_n >= 18 else 12
     if args.mode == "prove":
@@ -639,8 +745,8 @@ def main():
     if args.mode in ("ntt", "msm"):
         return run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n)
     shard = args.shard_msm and world > 1
-    if args.mode == "prove" and not shard:
-        return run_full(args, plk, torch, dist, world, rank, device, k, n)
+    if args.mode == "prove":
+        return run_full(args, plk, torch, dist, world, rank, device, k, n, shard)
     hp = HotPath(plk, torch, k, device, seed=1 if shard else 1000 * rank + 1, shard=shard)
     for _ in range(args.warmup):
         hp.step()
@@ -703,7 +809,7 @@ def main():
         },
         "breakdown_ms_per_step": {
             "ntt_n_x11": t_ntt_n, "ntt_8n_x8": t_ntt_8n, "msm_accumulate_4_batches": t_acc,
-            "other": ms_per_step - t_ntt_n - t_ntt_8n,
+            "other": ms_per_step - t_ntt_n - t_ntt_8n - t_acc,
         },
         "roofline": {
             "bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -718,8 +824,7 @@ def main():
         result["roofline"]["point_adds_per_s"] = adds / (launch_ms * 1e-3)
         result["roofline"]["valu"] = valu_roofline(adds / (launch_ms * 1e-3))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(k, hp.pp, threads)
+        result["cpu_baseline"] = cpu_baseline(k, hp.pp, cpu_threads(args))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

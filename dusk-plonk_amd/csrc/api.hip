@@ -400,7 +400,7 @@ int plk_commit_batch_dev(plk_srs* s, const plk_fr* const* d_coeffs, const size_t
       chk[k] = lens[base + k];
       use[k] = chk[k] < s->n ? chk[k] : s->n;
     }
-    const int r = msm_run_batch(s, ptrs, use, chk, m, outs + base, statuses ? statuses + base : nullptr, st);
+    const int r = msm_run_batch(s, *s->ws, ptrs, use, chk, m, outs + base, statuses ? statuses + base : nullptr, st);
     if (r != PLK_OK && r != PLK_E_DEGREE) return r;
     if (r != PLK_OK && overall == PLK_OK) overall = r;
   }
@@ -469,26 +469,26 @@ int plk_msm_sharded(plk_srs* const* per_gpu, int n_gpu, const plk_fr* scalars, s
 
 int plk_srs_msm_stats_reset(plk_srs* s) {
   if (!s) return PLK_E_ARG;
-  s->cum_accumulate_ms = 0.0;
-  s->cum_launches = s->cum_point_adds = s->cum_points = 0;
+  s->ws->stats.reset_cum();
   return PLK_OK;
 }
 
 int plk_srs_cum_msm_stats(const plk_srs* s, double* accumulate_ms, uint64_t* launches,
                           uint64_t* point_adds, uint64_t* points) {
   if (!s) return PLK_E_ARG;
-  if (accumulate_ms) *accumulate_ms = s->cum_accumulate_ms;
-  if (launches) *launches = s->cum_launches;
-  if (point_adds) *point_adds = s->cum_point_adds;
-  if (points) *points = s->cum_points;
+  const MsmStats& st = s->ws->stats;
+  if (accumulate_ms) *accumulate_ms = st.cum_accumulate_ms;
+  if (launches) *launches = st.cum_launches;
+  if (point_adds) *point_adds = st.cum_point_adds;
+  if (points) *points = st.cum_points;
   return PLK_OK;
 }
 
 int plk_srs_last_msm_stats(const plk_srs* s, float* accumulate_ms, uint64_t* point_adds,
                            uint32_t* window_bits) {
   if (!s) return PLK_E_ARG;
-  if (accumulate_ms) *accumulate_ms = s->last_accumulate_ms;
-  if (point_adds) *point_adds = s->last_point_adds;
+  if (accumulate_ms) *accumulate_ms = s->ws->stats.last_accumulate_ms;
+  if (point_adds) *point_adds = s->ws->stats.last_point_adds;
   if (window_bits) *window_bits = s->c;
   return PLK_OK;
 }

@@ -94,6 +94,20 @@ struct plk_domain {
 
 namespace plk {
 struct MsmWorkspace;
+// Bucket-accumulation statistics of one MSM workspace (measurement only): the most recent
+// batch and the cumulative figures since the last reset — k_accumulate time from
+// dispatch-stamped events, launches, point additions and MSM points (scalar counts).
+struct MsmStats {
+  float last_accumulate_ms = 0.f;
+  uint64_t last_point_adds = 0;
+  uint32_t last_slots = 0;
+  double cum_accumulate_ms = 0.0;
+  uint64_t cum_launches = 0, cum_point_adds = 0, cum_points = 0;
+  void reset_cum() {
+    cum_accumulate_ms = 0.0;
+    cum_launches = cum_point_adds = cum_points = 0;
+  }
+};
 }
 
 struct plk_srs {
@@ -107,14 +121,9 @@ struct plk_srs {
   plk::DevBuf table_inf;     // uint8, windows * n
   bool has_inf = false;      // any point at infinity in the SRS (slow-path flag checks)
   plk::DevBuf staging;       // host-scalar entry points stage through it
+  // the workspace of the SRS's own entry points (plk_msm / plk_commit*: one thread at a
+  // time); concurrent provers sharing this SRS each bring their own (plk_prover)
   std::unique_ptr<plk::MsmWorkspace> ws;
-  float last_accumulate_ms = 0.f;
-  uint64_t last_point_adds = 0;
-  uint32_t last_slots = 0;
-  // cumulative since plk_srs_msm_stats_reset: k_accumulate time (HIP events on the MSM's
-  // stream), launches, point additions and MSM points (sum of scalar counts)
-  double cum_accumulate_ms = 0.0;
-  uint64_t cum_launches = 0, cum_point_adds = 0, cum_points = 0;
   plk_srs();
   ~plk_srs();
 };
@@ -196,9 +205,15 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
 int msm_prepare_srs(plk_srs* s, hipStream_t stream);
 int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g1* out,
             hipStream_t stream);
-int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
+// The SRS (window table) is only read: any number of threads may run batches on one SRS
+// concurrently, each with its own workspace `w` and stream.
+int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const size_t* lens,
                   const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
                   hipStream_t stream);
+MsmWorkspace* msm_workspace_new();
+void msm_workspace_delete(MsmWorkspace* w);
+const MsmStats& msm_workspace_stats(const MsmWorkspace& w);
+MsmStats& msm_workspace_stats(MsmWorkspace& w);
 void fr_root_of_unity(uint32_t log_n, Fr& omega);
 int ntt_vanishing(plk_domain* d, uint64_t deg, Fr* d_out, hipStream_t s);
 int srs_generate(plk_srs* s, const Fr& tau_mont, uint64_t start, hipStream_t stream);

@@ -513,8 +513,7 @@ static G1xyzz rx_to_r_domain(const G1xyzz& p) {
   return r;
 }
 
-int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
-  MsmWorkspace& w = *s->ws;
+int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
   if (len <= w.cap_len && slots <= w.cap_slots && w.cap_len) return PLK_OK;
   len = std::max(len, w.cap_len);
   slots = std::max(slots, w.cap_slots);
@@ -555,7 +554,7 @@ int ws_reserve(plk_srs* s, size_t len, uint32_t slots) {
 // d_scalars[k][0 .. lens[k]) (lens[k] <= n_srs) against the SRS prefix, and if
 // check_lens[k] > lens[k] the tail [lens[k], check_lens[k]) must be zero (else that slot
 // reports PLK_E_DEGREE). statuses[k] receives each slot's status.
-int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
+int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const size_t* lens,
                   const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
                   hipStream_t stream) {
   if (count == 0) return PLK_OK;
@@ -573,8 +572,7 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
     total_entries += (size_t)s->windows * lens[k];
   }
   int st;
-  if ((st = ws_reserve(s, max_len ? max_len : 1, (uint32_t)count))) return st;
-  MsmWorkspace& w = *s->ws;
+  if ((st = ws_reserve(s, w, max_len ? max_len : 1, (uint32_t)count))) return st;
   const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1)};
   const uint32_t B = cfg.B;
   const uint32_t G = cdiv(B, 256);  // a power of two
@@ -665,15 +663,16 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
                              stream));
   PLK_HIP_TRY(hipMemcpyAsync(flag, w.flag.ptr, slots * 4, hipMemcpyDeviceToHost, stream));
   PLK_HIP_TRY(stream_wait(stream));
+  MsmStats& stt = w.stats;
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, w.ev0, w.ev1) == hipSuccess) s->last_accumulate_ms = ms;
-  s->last_point_adds = 0;
-  for (uint32_t k = 0; k < slots; ++k) s->last_point_adds += ent[k];
-  s->last_slots = slots;
-  s->cum_accumulate_ms += s->last_accumulate_ms;
-  s->cum_launches += 1;
-  s->cum_point_adds += s->last_point_adds;
-  for (uint32_t k = 0; k < slots; ++k) s->cum_points += batch.len[k];
+  if (hipEventElapsedTime(&ms, w.ev0, w.ev1) == hipSuccess) stt.last_accumulate_ms = ms;
+  stt.last_point_adds = 0;
+  for (uint32_t k = 0; k < slots; ++k) stt.last_point_adds += ent[k];
+  stt.last_slots = slots;
+  stt.cum_accumulate_ms += stt.last_accumulate_ms;
+  stt.cum_launches += 1;
+  stt.cum_point_adds += stt.last_point_adds;
+  for (uint32_t k = 0; k < slots; ++k) stt.cum_points += batch.len[k];
 
   int overall = PLK_OK;
   for (uint32_t k = 0; k < slots; ++k) {
@@ -705,8 +704,13 @@ int msm_run_batch(plk_srs* s, const Fr* const* d_scalars, const size_t* lens,
 
 int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g1* out,
             hipStream_t stream) {
-  return msm_run_batch(s, &d_scalars, &len, &check_len, 1, out, nullptr, stream);
+  return msm_run_batch(s, *s->ws, &d_scalars, &len, &check_len, 1, out, nullptr, stream);
 }
+
+MsmWorkspace* msm_workspace_new() { return new MsmWorkspace(); }
+void msm_workspace_delete(MsmWorkspace* w) { delete w; }
+const MsmStats& msm_workspace_stats(const MsmWorkspace& w) { return w.stats; }
+MsmStats& msm_workspace_stats(MsmWorkspace& w) { return w.stats; }
 
 }  // namespace plk
 

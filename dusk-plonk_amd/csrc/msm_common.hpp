@@ -80,12 +80,13 @@ struct MsmWorkspace {
   size_t cap_len = 0, task_stride = 0, sorted_stride = 0;
   uint32_t cap_slots = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  MsmStats stats;
   ~MsmWorkspace() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
   }
 };
 
-int ws_reserve(plk_srs* s, size_t len, uint32_t slots);
+int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots);
 
 }  // namespace plk

@@ -165,11 +165,28 @@ Gate gate_unpack(const plk_composer* c, size_t i) {
   return g;
 }
 
+inline uint64_t hash_mix(uint64_t h, uint64_t v) {
+  h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  return h * 0xff51afd7ed558ccdull;
+}
+
 int push_gate(plk_composer* c, const GateRec& g) {
   for (int k = 0; k < 4; ++k)
     if (g.w[k] >= c->witness.size()) return PLK_E_ARG;  // permutation.rs:98 assert
   const uint32_t n = (uint32_t)c->gates.size();
   c->gates.push_back(g);
+  {  // structure hash: wires, selector codes (incl. the PI bit) and pooled selector values
+    uint64_t h = hash_mix(c->struct_hash, (uint64_t)g.w[0] | ((uint64_t)g.w[1] << 32));
+    h = hash_mix(h, (uint64_t)g.w[2] | ((uint64_t)g.w[3] << 32));
+    h = hash_mix(h, g.code);
+    uint32_t e = g.ext;
+    for (int q = 0; q < 11; ++q)
+      if (sel_code(g.code, q) == kSelPooled) {
+        const Fr& v = c->consts[e++];
+        for (int i = 0; i < 8; i += 2) h = hash_mix(h, (uint64_t)v.v[i] | ((uint64_t)v.v[i + 1] << 32));
+      }
+    c->struct_hash = h;
+  }
   for (int k = 0; k < 4; ++k) {  // add_witnesses_to_map (permutation.rs:72-91)
     const uint32_t wire = 4 * n + k, wit = g.w[k];
     c->wire_next.push_back(plk_composer::kNoWire);
@@ -284,21 +301,97 @@ uint32_t log2_ceil(uint64_t x) {
   } while (0)
 
 // commit a batch of device polys against the key's trimmed SRS (key.rs:81-82): a poly whose
-// non-zero part is longer than the trimmed SRS fails with PLK_E_DEGREE.
-int key_commit(plk_key* key, const std::vector<const Fr*>& ptrs, const std::vector<size_t>& lens,
-               plk_g1* outs, int* statuses, hipStream_t s) {
+// non-zero part is longer than the trimmed SRS fails with PLK_E_DEGREE. `ws` / `s`: the
+// calling prover's MSM workspace and stream.
+int key_commit(plk_key* key, MsmWorkspace& ws, const std::vector<const Fr*>& ptrs,
+               const std::vector<size_t>& lens, plk_g1* outs, int* statuses, hipStream_t s) {
   const size_t max_points = std::min<size_t>(key->srs->n, key->n_trim);
   std::vector<size_t> use(lens.size());
   for (size_t i = 0; i < lens.size(); ++i) use[i] = std::min(lens[i], max_points);
   int overall = PLK_OK;
   for (size_t base = 0; base < ptrs.size(); base += kMaxSlots) {
     const size_t m = std::min<size_t>(kMaxSlots, ptrs.size() - base);
-    const int r = msm_run_batch(key->srs, ptrs.data() + base, use.data() + base, lens.data() + base,
-                                m, outs + base, statuses ? statuses + base : nullptr, s);
+    const int r = msm_run_batch(key->srs, ws, ptrs.data() + base, use.data() + base,
+                                lens.data() + base, m, outs + base,
+                                statuses ? statuses + base : nullptr, s);
     if (r != PLK_OK && r != PLK_E_DEGREE) return r;
     if (r != PLK_OK) overall = r;
   }
   return overall;
+}
+
+// The same commit group split over the ranks of a sharded prover (plk_prover_shard, SURVEY
+// §8e): this rank's MSMs over its SRS slice [lo, hi) of every polynomial, one all-gather
+// of (13 point words + status) per commit, and the fold of the partial points in rank order.
+// The last rank also checks the tail [max_points, len) for the degree error. Every rank
+// takes part in the exchange even when its own MSMs failed, so no rank waits forever on a
+// collective the others left.
+int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
+                 const std::vector<size_t>& lens, plk_g1* outs, int* statuses) {
+  plk_key* key = P->key;
+  const size_t cnt = ptrs.size();
+  const size_t max_points = std::min<size_t>(key->srs->n, key->n_trim);
+  const uint64_t lo = P->shard_lo, hi = lo + P->shard->n;
+  const bool last = P->rank == P->world - 1;
+  std::vector<const Fr*> lp(cnt);
+  std::vector<size_t> luse(cnt), lchk(cnt);
+  int local = PLK_OK;
+  if (last && hi < max_points) local = PLK_E_ARG;  // the slices do not cover the trimmed SRS
+  for (size_t i = 0; i < cnt; ++i) {
+    const size_t use = std::min(lens[i], max_points);
+    luse[i] = use > lo ? (size_t)(std::min<uint64_t>(use, hi) - lo) : 0;
+    lchk[i] = luse[i];
+    if (last && lens[i] > use) {
+      if (use < lo) local = PLK_E_ARG;  // the tail would start before this slice
+      else lchk[i] = lens[i] - lo;
+    }
+    lp[i] = ptrs[i] + lo;
+  }
+  std::vector<plk_g1> part(cnt, plk_g1{});
+  std::vector<int> pst(cnt, PLK_OK);
+  for (size_t base = 0; local == PLK_OK && base < cnt; base += kMaxSlots) {
+    const size_t m = std::min<size_t>(kMaxSlots, cnt - base);
+    const int r = msm_run_batch(P->shard, *P->ws, lp.data() + base, luse.data() + base,
+                                lchk.data() + base, m, part.data() + base, pst.data() + base,
+                                P->stream);
+    if (r != PLK_OK && r != PLK_E_DEGREE) local = r;
+  }
+  // payload per commit: x[6], y[6], infinity, status
+  constexpr size_t kWords = 14;
+  std::vector<uint64_t> send(cnt * kWords), recv((size_t)P->world * cnt * kWords);
+  for (size_t i = 0; i < cnt; ++i) {
+    uint64_t* w = &send[i * kWords];
+    std::memcpy(w, &part[i], sizeof(plk_g1));
+    w[13] = (uint64_t)(local != PLK_OK ? local : pst[i]);
+  }
+  if (P->allgather(P->allgather_user, send.data(), send.size() * 8, recv.data()) != 0)
+    return PLK_E_DEVICE;
+  int overall = PLK_OK;
+  std::vector<plk_g1> pts((size_t)P->world);
+  for (size_t i = 0; i < cnt; ++i) {
+    int st = PLK_OK;
+    for (int r = 0; r < P->world; ++r) {
+      const uint64_t* w = &recv[((size_t)r * cnt + i) * kWords];
+      std::memcpy(&pts[r], w, sizeof(plk_g1));
+      if (w[13] != PLK_OK && (st == PLK_OK || st == PLK_E_DEGREE)) st = (int)w[13];
+    }
+    if (st != PLK_OK && st != PLK_E_DEGREE) return st;  // a rank's device / argument error
+    if (statuses) statuses[i] = st;
+    if (st != PLK_OK) {
+      outs[i] = plk_g1{};
+      overall = PLK_E_DEGREE;
+      continue;
+    }
+    const int r = plk_g1_sum(pts.data(), pts.size(), &outs[i]);
+    if (r != PLK_OK) return r;
+  }
+  return overall;
+}
+
+int prover_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
+                  const std::vector<size_t>& lens, plk_g1* outs, int* statuses) {
+  if (P->world > 1) return shard_commit(P, ptrs, lens, outs, statuses);
+  return key_commit(P->key, *P->ws, ptrs, lens, outs, statuses, P->stream);
 }
 
 // JubJub twisted-Edwards d = -10240/10241 mod r
@@ -390,6 +483,7 @@ int plk_composer_destroy(plk_composer* c) {
   h->wire_head.clear();
   h->wire_tail.clear();
   h->wire_next.clear();
+  h->struct_hash = plk_composer::kHashInit;
   std::lock_guard<std::mutex> lk(g_pool_mu);
   if (g_pool.size() < kPoolMax) g_pool.push_back(std::move(h));
   return PLK_OK;
@@ -694,7 +788,7 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
       lens.push_back(n);
     }
     int sts[15];
-    const int r = key_commit(key.get(), ptrs, lens, key->comms, sts, s);
+    const int r = key_commit(key.get(), *srs->ws, ptrs, lens, key->comms, sts, s);
     if (r != PLK_OK && r != PLK_E_DEGREE) return r;
     for (int i = 0; i < 11; ++i)
       if (sts[i] != PLK_OK) key->comms[i] = plk_g1{{0}, {0}, 1};  // unwrap_or_default
@@ -741,7 +835,11 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     // 5. wire indices for the per-proof gather (prover.rs:114-119)
     std::vector<uint32_t> idx(4 * n, 0);
     for (uint64_t i = 0; i < m; ++i)
-      for (int c = 0; c < 4; ++c) idx[c * n + i] = cs->gates[i].w[c];
+      for (int c = 0; c < 4; ++c) {
+        idx[c * n + i] = cs->gates[i].w[c];
+        key->max_wire = std::max(key->max_wire, cs->gates[i].w[c]);
+      }
+    key->struct_hash = cs->struct_hash;
     TRY(key->wire_idx.alloc(4 * n * 4));
     PLK_HIP_TRY(hipMemcpyAsync(key->wire_idx.ptr, idx.data(), 4 * n * 4, hipMemcpyHostToDevice, s));
     PLK_HIP_TRY(stream_wait(s));
@@ -771,39 +869,124 @@ int plk_key_info(const plk_key* key, uint64_t* n, uint64_t* m, plk_g1* commitmen
 }
 
 // ----------------------------------------------------------------------- prover
+int plk_prover_create(plk_key* key, plk_prover** out) {
+  try {
+    if (!key || !out) return PLK_E_ARG;
+    *out = nullptr;
+    DeviceGuard guard(key->ctx->device);
+    std::unique_ptr<plk_prover> p(new plk_prover());
+    p->key = key;
+    p->ws = msm_workspace_new();
+    PLK_HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    p->own_stream = true;
+    *out = p.release();
+    return PLK_OK;
+  } catch (const std::bad_alloc&) {
+    return PLK_E_OOM;
+  }
+}
+
+int plk_prover_destroy(plk_prover* p) {
+  if (!p) return PLK_E_ARG;
+  DeviceGuard g(p->key->ctx->device);
+  (void)stream_wait(p->stream);
+  delete p;
+  return PLK_OK;
+}
+
+int plk_prover_stream(plk_prover* p, void** stream_out) {
+  if (!p || !stream_out) return PLK_E_ARG;
+  *stream_out = p->stream;
+  return PLK_OK;
+}
+
+int plk_prover_msm_stats(plk_prover* p, int reset, double* accumulate_ms, uint64_t* launches,
+                         uint64_t* point_adds, uint64_t* points) {
+  if (!p) return PLK_E_ARG;
+  MsmStats& st = msm_workspace_stats(*p->ws);
+  if (accumulate_ms) *accumulate_ms = st.cum_accumulate_ms;
+  if (launches) *launches = st.cum_launches;
+  if (point_adds) *point_adds = st.cum_point_adds;
+  if (points) *points = st.cum_points;
+  if (reset) st.reset_cum();
+  return PLK_OK;
+}
+
+int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int rank, int world,
+                     plk_allgather_fn allgather, void* user) {
+  if (!p || world < 1 || rank < 0 || rank >= world) return PLK_E_ARG;
+  if (world > 1 && (!slice || !allgather || slice->ctx->device != p->key->ctx->device))
+    return PLK_E_ARG;
+  p->shard = world > 1 ? slice : nullptr;
+  p->shard_lo = world > 1 ? slice_start : 0;
+  p->rank = rank;
+  p->world = world;
+  p->allgather = world > 1 ? allgather : nullptr;
+  p->allgather_user = user;
+  return PLK_OK;
+}
+
 int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* proof,
               plk_fr* public_inputs, size_t pi_cap, size_t* pi_count) {
+  if (!key) return PLK_E_ARG;
+  plk_prover* p;
+  {
+    std::lock_guard<std::mutex> lk(key->def_mu);
+    if (!key->def_prover) {
+      try {
+        std::unique_ptr<plk_prover> d(new plk_prover());
+        d->key = key;
+        d->ws = msm_workspace_new();
+        d->stream = key->ctx->stream;  // the context's stream, not owned
+        key->def_prover = std::move(d);
+      } catch (const std::bad_alloc&) {
+        return PLK_E_OOM;
+      }
+    }
+    p = key->def_prover.get();
+  }
+  return plk_prover_prove(p, cs, seed, proof, public_inputs, pi_cap, pi_count);
+}
+
+int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_proof* proof,
+                     plk_fr* public_inputs, size_t pi_cap, size_t* pi_count) {
   try {
-    if (!key || !cs || !proof) return PLK_E_ARG;
-    if (cs->gates.size() != key->m) return PLK_E_ARG;
+    if (!P || !cs || !proof) return PLK_E_ARG;
+    plk_key* key = P->key;
+    // the proving circuit must have the key's structure (prover.rs:114-119 gathers the
+    // wires of this circuit; the key's gather indices stand for them)
+    if (cs->gates.size() != key->m || cs->struct_hash != key->struct_hash) return PLK_E_ARG;
+    if (cs->witness.size() <= key->max_wire) return PLK_E_ARG;
     DeviceGuard guard(key->ctx->device);
-    hipStream_t s = key->ctx->stream;
+    hipStream_t s = P->stream;
     const uint64_t n = key->n, m = key->m, n8 = 8 * n, S = n + 8;  // S: padded poly stride
     Rng rng{seed};
     const Fr one = fe_one<FrCfg>();
     const Fr K1 = fr_u64(7), K2 = fr_u64(13), K3 = fr_u64(17);
 
-    // scratch (allocated once per key)
-    TRY(key->witness.alloc(std::max<size_t>(cs->witness.size(), 1) * sizeof(Fr)));
-    TRY(key->wires_lag.alloc(4 * n * sizeof(Fr)));
-    TRY(key->wires_coef.alloc(4 * S * sizeof(Fr)));
-    TRY(key->z_lag.alloc(n * sizeof(Fr)));
-    TRY(key->z_coef.alloc(S * sizeof(Fr)));
-    TRY(key->num.alloc(n * sizeof(Fr)));
-    TRY(key->den.alloc(n * sizeof(Fr)));
-    TRY(key->scan_tmp.alloc((pk_scan_tmp_elems(5 * n) + 1) * sizeof(Fr)));
-    TRY(key->pi_lag.alloc(n * sizeof(Fr)));
-    TRY(key->pi_coef.alloc(n * sizeof(Fr)));
-    TRY(key->ev8.alloc(6 * n8 * sizeof(Fr)));
-    TRY(key->quot8.alloc(n8 * sizeof(Fr)));
-    TRY(key->t_coef.alloc(n8 * sizeof(Fr)));
-    TRY(key->r_coef.alloc(S * sizeof(Fr)));
-    TRY(key->agg.alloc(5 * n * sizeof(Fr)));
-    TRY(key->agg2.alloc(S * sizeof(Fr)));
-    TRY(key->w_coef.alloc((5 * n + S) * sizeof(Fr)));
-    TRY(key->tmp_a.alloc(5 * n * sizeof(Fr)));
-    TRY(key->eval_partial.alloc((size_t)kMaxEval * pk_eval_max_blocks(n8) * sizeof(Fr)));
-    TRY(key->eval_out.alloc(kMaxEval * sizeof(Fr)));
+    // scratch (allocated once per prover)
+    TRY(P->witness.alloc(std::max<size_t>(cs->witness.size(), 1) * sizeof(Fr)));
+    TRY(P->wires_lag.alloc(4 * n * sizeof(Fr)));
+    TRY(P->wires_coef.alloc(4 * S * sizeof(Fr)));
+    TRY(P->z_lag.alloc(n * sizeof(Fr)));
+    TRY(P->z_coef.alloc(S * sizeof(Fr)));
+    TRY(P->num.alloc(n * sizeof(Fr)));
+    TRY(P->den.alloc(n * sizeof(Fr)));
+    TRY(P->scan_tmp.alloc((pk_scan_tmp_elems(5 * n) + 1) * sizeof(Fr)));
+    TRY(P->pi_lag.alloc(n * sizeof(Fr)));
+    TRY(P->pi_coef.alloc(n * sizeof(Fr)));
+    TRY(P->ev8.alloc(6 * n8 * sizeof(Fr)));
+    TRY(P->quot8.alloc(n8 * sizeof(Fr)));
+    TRY(P->t_coef.alloc(n8 * sizeof(Fr)));
+    TRY(P->r_coef.alloc(S * sizeof(Fr)));
+    TRY(P->agg.alloc(5 * n * sizeof(Fr)));
+    TRY(P->agg2.alloc(S * sizeof(Fr)));
+    TRY(P->w_coef.alloc((5 * n + S) * sizeof(Fr)));
+    TRY(P->tmp_a.alloc(5 * n * sizeof(Fr)));
+    TRY(P->eval_partial.alloc((size_t)kMaxEval * pk_eval_max_blocks(n8) * sizeof(Fr)));
+    TRY(P->eval_out.alloc(kMaxEval * sizeof(Fr)));
+    TRY(P->ntt_scratch.alloc(2 * n8 * sizeof(Fr)));
+    Fr* nsc = P->ntt_scratch.as<Fr>();
 
     // transcript seeded like Prover::new (prover.rs:54-55): Transcript::base(label, vk, m)
     Transcript tr(key->label);
@@ -829,22 +1012,22 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     {  // witness upload through pinned staging, in chunks: the CPU copy of chunk i+1
        // overlaps the DMA of chunk i (the previous proof's DMA finished at its last wait)
       const size_t bytes = cs->witness.size() * sizeof(Fr);
-      TRY(key->pin_witness.alloc(bytes));
+      TRY(P->pin_witness.alloc(bytes));
       const size_t chunk = 8u << 20;
       const char* src = reinterpret_cast<const char*>(cs->witness.data());
-      char* pin = key->pin_witness.as<char>();
-      char* dst = key->witness.as<char>();
+      char* pin = P->pin_witness.as<char>();
+      char* dst = P->witness.as<char>();
       for (size_t off = 0; off < bytes; off += chunk) {
         const size_t len = std::min(chunk, bytes - off);
         std::memcpy(pin + off, src + off, len);
         PLK_HIP_TRY(hipMemcpyAsync(dst + off, pin + off, len, hipMemcpyHostToDevice, s));
       }
     }
-    Fr* wl = key->wires_lag.as<Fr>();
-    Fr* wc = key->wires_coef.as<Fr>();
-    TRY(pk_gather_wires(key->witness.as<Fr>(), key->wire_idx.as<uint32_t>(), m, n, wl, s));
+    Fr* wl = P->wires_lag.as<Fr>();
+    Fr* wc = P->wires_coef.as<Fr>();
+    TRY(pk_gather_wires(P->witness.as<Fr>(), key->wire_idx.as<uint32_t>(), m, n, wl, s));
     for (int c = 0; c < 4; ++c) {
-      TRY(ntt_run(key->dom, wl + c * n, wc + c * S, n, -1, 0, nullptr, s, 1));
+      TRY(ntt_run(key->dom, wl + c * n, wc + c * S, n, -1, 0, nsc, s, 1));
       BlindArgs b{};
       b.count = 2;
       b.r[0] = rng.fr();
@@ -852,8 +1035,8 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       TRY(pk_blind(wc + c * S, n, b, s));
     }
     plk_g1 wcom[4];
-    TRY(key_commit(key, {wc, wc + S, wc + 2 * S, wc + 3 * S}, {n + 2, n + 2, n + 2, n + 2}, wcom,
-                   nullptr, s));
+    TRY(prover_commit(P, {wc, wc + S, wc + 2 * S, wc + 3 * S}, {n + 2, n + 2, n + 2, n + 2}, wcom,
+                      nullptr));
     tr.append_commitment("a_w", wcom[0]);
     tr.append_commitment("b_w", wcom[1]);
     tr.append_commitment("c_w", wcom[2]);
@@ -863,18 +1046,18 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     const Fr beta = tr.challenge_scalar("beta");
     tr.append_scalar("beta", beta);
     const Fr gamma = tr.challenge_scalar("gamma");
-    Fr* num = key->num.as<Fr>();
-    Fr* den = key->den.as<Fr>();
+    Fr* num = P->num.as<Fr>();
+    Fr* den = P->den.as<Fr>();
     TRY(pk_perm_numden(wl, key->sigma_lag.as<Fr>(), key->dom->tw_fwd.as<Fr>(), n, beta, gamma, K1,
                        K2, K3, num, den, s));
-    Fr* st = key->scan_tmp.as<Fr>();
+    Fr* st = P->scan_tmp.as<Fr>();
     TRY(pk_scan(num, num, n, true, false, true, st, s));   // N_i = prod_{j<i} num_j
     TRY(pk_scan(den, den, n, true, true, false, st, s));   // S_i = prod_{j>=i} den_j
     const uint64_t nb = pk_scan_tmp_elems(n) - 1;
     const Fr dtot = d2h_fr(st + nb, s);                    // prod of all den_j
-    TRY(pk_mul3(num, den, fe_inv(dtot), key->z_lag.as<Fr>(), n, s));
-    Fr* zc = key->z_coef.as<Fr>();
-    TRY(ntt_run(key->dom, key->z_lag.as<Fr>(), zc, n, -1, 0, nullptr, s, 1));
+    TRY(pk_mul3(num, den, fe_inv(dtot), P->z_lag.as<Fr>(), n, s));
+    Fr* zc = P->z_coef.as<Fr>();
+    TRY(ntt_run(key->dom, P->z_lag.as<Fr>(), zc, n, -1, 0, nsc, s, 1));
     {
       BlindArgs b{};
       b.count = 3;
@@ -882,7 +1065,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       TRY(pk_blind(zc, n, b, s));
     }
     plk_g1 zcom;
-    TRY(key_commit(key, {zc}, {n + 3}, &zcom, nullptr, s));
+    TRY(prover_commit(P, {zc}, {n + 3}, &zcom, nullptr));
     tr.append_commitment("z", zcom);
 
     // ---- round 3: quotient (prover.rs:201-287, quotient_poly.rs)
@@ -891,27 +1074,27 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     const Fr logic_sep = tr.challenge_scalar("logic separation challenge");
     const Fr fixed_sep = tr.challenge_scalar("fixed base separation challenge");
     const Fr var_sep = tr.challenge_scalar("variable base separation challenge");
-    Fr* pil = key->pi_lag.as<Fr>();
+    Fr* pil = P->pi_lag.as<Fr>();
     if (!pis.empty()) PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
     // pin_small: [0, #pi) PI values uploaded here, [#pi, #pi + 16) the evaluations read
     // back in round 4 (sized once: queued copies keep pointing into it)
-    TRY(key->pin_small.alloc((pis.size() + 16) * sizeof(Fr)));
+    TRY(P->pin_small.alloc((pis.size() + 16) * sizeof(Fr)));
     for (size_t i = 0; i < pis.size(); ++i) {
-      key->pin_small.as<Fr>()[i] = pis[i].second;
-      PLK_HIP_TRY(hipMemcpyAsync(pil + pis[i].first, key->pin_small.as<Fr>() + i, sizeof(Fr),
+      P->pin_small.as<Fr>()[i] = pis[i].second;
+      PLK_HIP_TRY(hipMemcpyAsync(pil + pis[i].first, P->pin_small.as<Fr>() + i, sizeof(Fr),
                                  hipMemcpyHostToDevice, s));
     }
-    Fr* ev = key->ev8.as<Fr>();  // z, a, b, c, d, pi over the 8n coset
-    if (!pis.empty()) TRY(ntt_run(key->dom, pil, key->pi_coef.as<Fr>(), n, -1, 0, nullptr, s, 1));
-    TRY(ntt_run(key->dom8, zc, ev + 0 * n8, n + 3, 1, 1, nullptr, s, 1));
+    Fr* ev = P->ev8.as<Fr>();  // z, a, b, c, d, pi over the 8n coset
+    if (!pis.empty()) TRY(ntt_run(key->dom, pil, P->pi_coef.as<Fr>(), n, -1, 0, nsc, s, 1));
+    TRY(ntt_run(key->dom8, zc, ev + 0 * n8, n + 3, 1, 1, nsc, s, 1));
     // wire evaluations at exponent -1 and PI at +1 for k_quotient's redundant-form
     // arithmetic (QuotientArgs): scaled coset tables, no extra pass
     for (int c = 0; c < 4; ++c)
-      TRY(ntt_run(key->dom8, wc + c * S, ev + (1 + c) * n8, n + 2, 1, 1, nullptr, s, 1,
+      TRY(ntt_run(key->dom8, wc + c * S, ev + (1 + c) * n8, n + 2, 1, 1, nsc, s, 1,
                   key->coset_w.as<Fr>()));
     // PI(X) over the coset; a circuit without public inputs has PI = 0 (the term is skipped)
     if (!pis.empty())
-      TRY(ntt_run(key->dom8, key->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nullptr, s, 1,
+      TRY(ntt_run(key->dom8, P->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nsc, s, 1,
                   key->coset_pi.as<Fr>()));
     const Fr alpha2 = fe_sqr(alpha);
     QuotientArgs qa{};
@@ -926,7 +1109,7 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     qa.sel = key->sel8.as<Fr>();
     qa.sigma = key->sigma8.as<Fr>();
     qa.elements8 = key->dom8->tw_fwd.as<Fr>();
-    qa.out = key->quot8.as<Fr>();
+    qa.out = P->quot8.as<Fr>();
     qa.n8 = n8;
     qa.g = key->dom8->g;
     qa.alpha = alpha;
@@ -976,13 +1159,13 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       qa.rx_inv32 = fe_inv(qa.rx_32);
     }
     TRY(pk_quotient(qa, s));
-    Fr* tc = key->t_coef.as<Fr>();
-    TRY(ntt_run(key->dom8, key->quot8.as<Fr>(), tc, n8, -1, 1, nullptr, s, 1));
+    Fr* tc = P->t_coef.as<Fr>();
+    TRY(ntt_run(key->dom8, P->quot8.as<Fr>(), tc, n8, -1, 1, nsc, s, 1));
     // split into t_low, t_mid, t_high (n each) and t_4 = t[3n..] (prover.rs:252-265)
     plk_g1 tcom[4];
-    TRY(key_commit(key, {tc, tc + n, tc + 2 * n, tc + 3 * n}, {n, n, n, 5 * n}, tcom, nullptr, s));
+    TRY(prover_commit(P, {tc, tc + n, tc + 2 * n, tc + 3 * n}, {n, n, n, 5 * n}, tcom, nullptr));
     // t_4 is 5n coefficients in the reference (prover.rs:259); its commit succeeded, so
-    // everything past the committed SRS prefix is zero (key_commit checks the tail): t and
+    // everything past the committed SRS prefix is zero (the commit checks the tail): t and
     // t_4 end at 3n + t4_len for the evaluation and the opening below
     const uint64_t t4_len = std::min<uint64_t>(5 * n, std::min<uint64_t>(key->srs->n, key->n_trim));
     tr.append_commitment("t_low", tcom[0]);
@@ -1006,10 +1189,10 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       eb.len[i] = lens[i];
       eb.x[i] = i < 12 ? zeta : zw;
     }
-    TRY(pk_eval(eb, 16, 3 * n + t4_len, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
+    TRY(pk_eval(eb, 16, 3 * n + t4_len, P->eval_partial.as<Fr>(), P->eval_out.as<Fr>(), s));
     Fr evs[16];
-    Fr* evs_pin = key->pin_small.as<Fr>() + pis.size();
-    PLK_HIP_TRY(hipMemcpyAsync(evs_pin, key->eval_out.ptr, sizeof evs, hipMemcpyDeviceToHost, s));
+    Fr* evs_pin = P->pin_small.as<Fr>() + pis.size();
+    PLK_HIP_TRY(hipMemcpyAsync(evs_pin, P->eval_out.ptr, sizeof evs, hipMemcpyDeviceToHost, s));
     PLK_HIP_TRY(stream_wait(s));
     std::memcpy(evs, evs_pin, sizeof evs);
     const Fr t_eval = evs[0], a_e = evs[1], b_e = evs[2], c_e = evs[3], d_e = evs[4];
@@ -1082,14 +1265,14 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     cpc = fe_mul(cpc, fe_add(fe_add(c_e, fe_mul(beta, s3_e)), gamma));
     cpc = fe_mul(fe_mul(cpc, fe_mul(beta, perm_e)), alpha);
     term(sc + 3 * n, n, fe_neg(cpc));
-    Fr* rc = key->r_coef.as<Fr>();
+    Fr* rc = P->r_coef.as<Fr>();
     TRY(pk_lincomb(lc, rc, n + 3, s));
     EvalBatch er{};
     er.poly[0] = rc;
     er.len[0] = n + 3;
     er.x[0] = zeta;
-    TRY(pk_eval(er, 1, n + 3, key->eval_partial.as<Fr>(), key->eval_out.as<Fr>(), s));
-    const Fr r_e = d2h_fr(key->eval_out.as<Fr>(), s);
+    TRY(pk_eval(er, 1, n + 3, P->eval_partial.as<Fr>(), P->eval_out.as<Fr>(), s));
+    const Fr r_e = d2h_fr(P->eval_out.as<Fr>(), s);
 
     const char* elabels[17] = {"a_eval", "b_eval", "c_eval", "d_eval", "a_next_eval",
                                "b_next_eval", "d_next_eval", "s_sigma_1_eval", "s_sigma_2_eval",
@@ -1129,11 +1312,11 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
       vp = fe_mul(vp, v1);
       lt(sc + c * n, n, vp);
     }
-    Fr* ag = key->agg.as<Fr>();
+    Fr* ag = P->agg.as<Fr>();
     TRY(pk_lincomb(la, ag, agg_len, s));
-    Fr* w1 = key->w_coef.as<Fr>();
+    Fr* w1 = P->w_coef.as<Fr>();
     Fr* w2 = w1 + 5 * n;
-    TRY(pk_ruffini(ag, agg_len, zeta, w1, key->tmp_a.as<Fr>(), st, s));
+    TRY(pk_ruffini(ag, agg_len, zeta, w1, P->tmp_a.as<Fr>(), st, s));
     // W'(X) = (z + v2 a + v2^2 b + v2^3 d) / (X - z w)
     LinComb lb{};
     lb.terms = 4;
@@ -1149,11 +1332,11 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
     lb.p[3] = wc + 3 * S;
     lb.len[3] = n + 2;
     lb.s[3] = fe_mul(lb.s[2], v2);
-    Fr* ag2 = key->agg2.as<Fr>();
+    Fr* ag2 = P->agg2.as<Fr>();
     TRY(pk_lincomb(lb, ag2, n + 3, s));
-    TRY(pk_ruffini(ag2, n + 3, zw, w2, key->tmp_a.as<Fr>(), st, s));
+    TRY(pk_ruffini(ag2, n + 3, zw, w2, P->tmp_a.as<Fr>(), st, s));
     plk_g1 wcm[2];
-    TRY(key_commit(key, {w1, w2}, {agg_len - 1, n + 2}, wcm, nullptr, s));
+    TRY(prover_commit(P, {w1, w2}, {agg_len - 1, n + 2}, wcm, nullptr));
 
     // ---- proof (proof.rs:36-66)
     proof->a_comm = wcom[0];
@@ -1192,3 +1375,10 @@ int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* pr
 }
 
 }  // extern "C"
+
+plk_prover::~plk_prover() {
+  if (own_stream && stream) (void)hipStreamDestroy(stream);
+  plk::msm_workspace_delete(ws);
+}
+
+plk_key::~plk_key() = default;

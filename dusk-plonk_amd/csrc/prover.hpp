@@ -179,6 +179,11 @@ struct plk_composer {
   // per wire; kNoWire terminates.
   static constexpr uint32_t kNoWire = 0xffffffffu;
   std::vector<uint32_t> wire_head, wire_tail, wire_next;
+  // running hash of the circuit's structure (every gate's wires, selector codes, pooled
+  // selector values and public-input position — not witness or public-input values),
+  // updated as gates are appended: plk_prove compares it with the key's in O(1)
+  static constexpr uint64_t kHashInit = 0x6a09e667f3bcc908ull;
+  uint64_t struct_hash = kHashInit;
 };
 
 struct plk_key {
@@ -202,8 +207,34 @@ struct plk_key {
   plk::DevBuf wire_idx;     // 4 x n witness indices per gate (u32)
   plk::Fr vh_inv[8];
   plk_g1 comms[15];         // q_m q_l q_r q_o q_c q_4 q_arith q_range q_logic q_fixed q_var s1..s4
+  // the circuit the key was compiled from: plk_prove refuses a circuit whose structure hash
+  // differs or whose witness vector does not cover the largest wire index (prover.rs:114-119
+  // reads the wires of the proving circuit; the key's gather indices must be valid for it)
+  uint64_t struct_hash = 0;
+  uint32_t max_wire = 0;
+  // the prover behind plk_prove(key, ...) (context stream), created on first use
+  std::mutex def_mu;
+  std::unique_ptr<plk_prover> def_prover;
+  ~plk_key();
+};
+
+// One concurrent prover over a key (include/plk.h plk_prover): stream, MSM workspace, NTT
+// scratch and per-proof buffers of its own; the key and the SRS window table are shared
+// read-only by every prover of the key.
+struct plk_prover {
+  plk_key* key = nullptr;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  plk::MsmWorkspace* ws = nullptr;  // owned (msm_workspace_new)
+  // sharded commits (plk_prover_shard): this rank's SRS slice and the all-gather
+  plk_srs* shard = nullptr;
+  uint64_t shard_lo = 0;
+  int rank = 0, world = 1;
+  plk_allgather_fn allgather = nullptr;
+  void* allgather_user = nullptr;
   // per-proof scratch
   plk::PinnedBuf pin_witness, pin_small;  // host staging of the witness upload / small readbacks
-  plk::DevBuf witness, wires_lag, wires_coef, z_lag, z_coef, num, den, tmp_a, tmp_b, scan_tmp,
-      pi_lag, pi_coef, ev8, quot8, t_coef, r_coef, agg, agg2, w_coef, eval_partial, eval_out;
+  plk::DevBuf witness, wires_lag, wires_coef, z_lag, z_coef, num, den, tmp_a, scan_tmp, pi_lag,
+      pi_coef, ev8, quot8, t_coef, r_coef, agg, agg2, w_coef, eval_partial, eval_out, ntt_scratch;
+  ~plk_prover();
 };

@@ -8,6 +8,13 @@ every rank folds the partials on the host (``plk_g1_sum``): EC addition is not a
 reduction op, so the "all-reduce of partial sums" is an all-gather plus a local fold.
 Batches of independent commits (the prover's commit groups) share one all-gather.
 Proof batches need no collective at all (bench.py default mode).
+
+The full prover uses the same split inside ``plk_prover_prove`` (BASELINE configs[4]):
+``shard_prover_lane`` gives a prover lane its SRS slice and a torch.distributed all-gather
+as the C ABI's ``plk_allgather_fn``; every rank then proves the same circuit with the same
+seed, runs the NTT / elementwise rounds as replicas and splits each of the proof's 4 commit
+groups (wires, z, quotient chunks, openings: prover.rs:133-136,194,262-265,440,452) by SRS
+index — one all-gather of 14 words per commit per group, host fold on every rank.
 """
 from __future__ import annotations
 
@@ -44,6 +51,45 @@ def gather_fold(partials: np.ndarray, statuses, group=None, device=None) -> list
         st = int(allp[:, k, 13].max())
         res.append(g1_sum(allp[:, k, :13]) if st == PLK_OK else PlonkError(st, "sharded commit"))
     return res
+
+
+def torch_allgather(group=None, device=None):
+    """`allgather(send: bytes) -> bytes` over a torch.distributed group: every rank's
+    bytes concatenated in rank order (all_gather_into_tensor; on `device` for RCCL, on the
+    host under gloo). The byte-level collective behind plk_allgather_fn."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+
+    def allgather(data: bytes) -> bytes:
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(device or "cpu")
+        out = torch.empty(world * len(data), dtype=torch.uint8, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=group)
+        return out.cpu().numpy().tobytes()
+
+    return allgather
+
+
+def srs_slice(tau, n_points: int, world: int, rank: int, ctx=None):
+    """(slice start, PlonkParams) of rank `rank`'s share of the first `n_points` SRS
+    powers of `tau` (plk_srs_setup_range on its GPU, window table included)."""
+    lo, hi = shard_range(n_points, world, rank)
+    return lo, PlonkParams.setup_range(tau, lo, hi - lo, ctx)
+
+
+def shard_prover_lane(lane, tau, n_points: int, group=None, device=None, ctx=None,
+                      slice_=None):
+    """Split every commit of `lane` (a prover.ProverLane) over the ranks of `group`: this
+    rank's slice of the first `n_points` SRS powers of `tau` and the group's all-gather.
+    `slice_` = (start, PlonkParams) from srs_slice lets several lanes share one slice (the
+    SRS is read-only; each lane brings its own MSM workspace). Returns the slice."""
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, sl = slice_ if slice_ is not None else srs_slice(tau, n_points, world, rank, ctx)
+    lane.shard(sl, lo, rank, world, torch_allgather(group, device))
+    return lo, sl
 
 
 class ShardedPlonkParams:
@@ -92,4 +138,5 @@ class ShardedPlonkParams:
         return r
 
 
-__all__ = ["ShardedPlonkParams", "gather_fold", "shard_range", "PLK_E_DEGREE"]
+__all__ = ["ShardedPlonkParams", "gather_fold", "shard_range", "shard_prover_lane",
+           "srs_slice", "torch_allgather", "PLK_E_DEGREE"]

@@ -51,6 +51,11 @@ class PlkProof(C.Structure):
     _fields_ = [(c, PlkG1) for c in _COMMS] + [(e, PlkFr) for e in _EVALS]
 
 
+# plk_allgather_fn (include/plk.h): (user, send, bytes, recv) -> 0 on success
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+PROOF_SCALE_BYTES = 11 * 97 + 16 * 32  # PLK_PROOF_SCALE_BYTES
+
+
 def _bind():
     lib = _lib()
     if getattr(lib, "_prover_bound", False):
@@ -76,6 +81,14 @@ def _bind():
         "plk_key_compile": [vp, vp, C.c_char_p, pp], "plk_key_destroy": [vp],
         "plk_key_info": [vp, C.POINTER(u64), C.POINTER(u64), vp],
         "plk_prove": [vp, vp, u64, vp, vp, sz, C.POINTER(sz)],
+        "plk_prover_create": [vp, pp], "plk_prover_destroy": [vp],
+        "plk_prover_stream": [vp, pp],
+        "plk_prover_prove": [vp, vp, u64, vp, vp, sz, C.POINTER(sz)],
+        "plk_prover_msm_stats": [vp, i32, C.POINTER(C.c_double), C.POINTER(u64),
+                                 C.POINTER(u64), C.POINTER(u64)],
+        "plk_prover_shard": [vp, vp, u64, i32, i32, vp, vp],  # fn: ALLGATHER_FN cast
+        "plk_proof_encode": [vp, vp, sz, C.POINTER(sz)],
+        "plk_proof_decode": [vp, sz, vp],
     }
     for name, args in sig.items():
         f = getattr(lib, name)
@@ -239,6 +252,12 @@ class Plonk:
         g = C.c_size_t()
         _check(_bind().plk_composer_size(self._h, C.byref(g), None), "size")
         return g.value
+
+    def set_witness(self, w: int, v):
+        """Overwrite witness `w` (plk_composer_set_witness): a new instance of the same
+        circuit structure."""
+        f = _fr(v)
+        _check(_bind().plk_composer_set_witness(self._h, w, C.byref(f)), "set_witness")
 
     def append_witness(self, v) -> int:
         w = C.c_uint32()
@@ -500,7 +519,38 @@ class Proof:
             setattr(self, e, fr_int(getattr(raw, e)))
 
     def to_bytes(self) -> bytes:
+        """The SCALE encoding of the reference's ``Proof`` (``#[derive(Encode)]``,
+        src/prover/proof.rs:11,36): 11 commitments then the 16 evaluations, with the
+        element encodings ASSUMED as documented at plk_proof_encode (include/plk.h)."""
+        out = (C.c_uint8 * PROOF_SCALE_BYTES)()
+        n = C.c_size_t()
+        _check(_bind().plk_proof_encode(C.byref(self.raw), out, PROOF_SCALE_BYTES, C.byref(n)),
+               "Proof::encode")
+        return bytes(out[: n.value])
+
+    @staticmethod
+    def from_bytes(data: bytes) -> "Proof":
+        """``Proof::decode`` of :meth:`to_bytes` output; raises PlonkError(PLK_E_ARG) on a
+        wrong length, a non-boolean infinity byte, non-canonical limbs or an off-curve point."""
+        raw = PlkProof()
+        buf = (C.c_uint8 * len(data)).from_buffer_copy(data) if data else None
+        _check(_bind().plk_proof_decode(buf, len(data), C.byref(raw)), "Proof::decode")
+        return Proof(raw)
+
+    @staticmethod
+    def from_words(comms, evals) -> "Proof":
+        """A Proof from uint64 arrays: comms (11, 13) ABI points, evals (16, 4) Montgomery."""
+        c = np.ascontiguousarray(comms, dtype=np.uint64).reshape(11, 13)
+        e = np.ascontiguousarray(evals, dtype=np.uint64).reshape(16, 4)
+        raw = PlkProof.from_buffer_copy(c.tobytes() + e.tobytes())
+        return Proof(raw)
+
+    def raw_bytes(self) -> bytes:
+        """The in-memory plk_proof struct (104-byte ABI points, Montgomery limbs)."""
         return bytes(self.raw)
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, Proof) and self.raw_bytes() == other.raw_bytes()
 
 
 class VerifierData:
@@ -529,10 +579,97 @@ class Prover:
             raise PlonkError(st, "create_proof")
         return Proof(proof), [fr_int(pis[i]) for i in range(cnt.value)]
 
+    def lane(self) -> "ProverLane":
+        """A concurrent prover over this key (plk_prover_create): own stream, MSM workspace
+        and scratch; the key and the SRS window table are shared, not copied. Lanes may
+        prove from different threads at once (``Prover: Clone`` in the reference)."""
+        return ProverLane(self)
+
     def __del__(self):
         try:
+            for ln in list(getattr(self, "_lanes", [])):
+                ln.close()
             if self._key:
                 _bind().plk_key_destroy(self._key)
+        except Exception:
+            pass
+
+
+class ProverLane:
+    """One plk_prover: create_proof on its own stream, sharing the key of `prover`."""
+
+    def __init__(self, prover: Prover):
+        self.prover = prover
+        self._h = C.c_void_p()
+        _check(_bind().plk_prover_create(prover._key, C.byref(self._h)), "plk_prover_create")
+        if not hasattr(prover, "_lanes"):
+            prover._lanes = []
+        prover._lanes.append(self)
+        self._shard_keep = None
+
+    @property
+    def stream(self) -> int:
+        s = C.c_void_p()
+        _check(_bind().plk_prover_stream(self._h, C.byref(s)), "plk_prover_stream")
+        return s.value or 0
+
+    def shard(self, slice_params, slice_start: int, rank: int, world: int, allgather):
+        """Split every commit of this lane's proofs over `world` ranks (plk_prover_shard):
+        `slice_params` is this rank's PlonkParams slice (PlonkParams.setup_range) starting
+        at SRS index `slice_start`; `allgather(send: bytes) -> bytes` returns the
+        concatenation of every rank's `send` in rank order."""
+        def cb(_user, send, nbytes, recv):
+            try:
+                data = allgather(C.string_at(send, nbytes))
+                if len(data) != world * nbytes:
+                    return 1
+                C.memmove(recv, data, len(data))
+                return 0
+            except Exception:  # noqa: BLE001 — reported to the prover as PLK_E_DEVICE
+                import traceback
+                traceback.print_exc()
+                return 1
+        fn = ALLGATHER_FN(cb)
+        self._shard_keep = (fn, slice_params)  # keep the callback and the slice alive
+        _check(_bind().plk_prover_shard(self._h, slice_params._h if slice_params else None,
+                                        slice_start, rank, world, C.cast(fn, C.c_void_p), None),
+               "plk_prover_shard")
+
+    def prove_composer(self, cs: Plonk, seed: int):
+        proof = PlkProof()
+        pis = (PlkFr * 4096)()
+        cnt = C.c_size_t()
+        st = _bind().plk_prover_prove(self._h, cs._h, seed, C.byref(proof), pis, 4096,
+                                      C.byref(cnt))
+        if st != PLK_OK:
+            raise PlonkError(st, "create_proof")
+        return Proof(proof), [fr_int(pis[i]) for i in range(cnt.value)]
+
+    def create_proof(self, seed: int, circuit):
+        cs = Plonk()
+        circuit.synthesize(cs)
+        return self.prove_composer(cs, seed)
+
+    def msm_stats(self, reset: bool = False):
+        """(k_accumulate ms, launches, point additions, MSM points) since the last reset."""
+        ms, la, ad, pt = C.c_double(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(_bind().plk_prover_msm_stats(self._h, 1 if reset else 0, C.byref(ms),
+                                            C.byref(la), C.byref(ad), C.byref(pt)),
+               "plk_prover_msm_stats")
+        return ms.value, la.value, ad.value, pt.value
+
+    def close(self):
+        if self._h:
+            _bind().plk_prover_destroy(self._h)
+            self._h = C.c_void_p()
+            try:
+                self.prover._lanes.remove(self)
+            except (AttributeError, ValueError):
+                pass
+
+    def __del__(self):
+        try:
+            self.close()
         except Exception:
             pass
 

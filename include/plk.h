@@ -4,8 +4,9 @@
  * This is the drop-in boundary. In the reference the path sits behind Rust generic
  * structs of un-vendored crates (no FFI exists there); each entry point
  * below replaces one of those calls. The host-side mirror that calls this ABI with the
- * reference's names is dusk-plonk_amd/plonk.py (Python, used by the tests) and
- * dusk-plonk_amd/csrc/plonk.hpp (C++). INTEGRATION.md shows the Rust-side binding.
+ * reference's names is dusk-plonk_amd/plonk.py + dusk-plonk_amd/prover.py (Python, used by
+ * the tests and bench.py); the C++ prover behind plk_prove is dusk-plonk_amd/csrc/prover.hip.
+ * INTEGRATION.md shows the Rust-side binding.
  *
  * Conventions
  *  - plk_fr is BlsScalar exactly as the reference stores it: 4 little-endian u64 limbs
@@ -30,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PLK_ABI_VERSION 1
+#define PLK_ABI_VERSION 2
 
 typedef struct { uint64_t l[4]; } plk_fr;                          /* 32 bytes  */
 typedef struct { uint64_t x[6]; uint64_t y[6]; uint64_t infinity; } plk_g1; /* 104 bytes */
@@ -228,9 +229,64 @@ int plk_key_destroy(plk_key* key);
 int plk_key_info(const plk_key* key, uint64_t* n, uint64_t* m, plk_g1* commitments);
 /* Prover::create_proof (src/prover.rs:67-474) for a circuit with the key's structure and
  * its own witness values. Blinding randomness comes from `seed` (SplitMix64). Fails with
- * PLK_E_DEGREE exactly where the reference's commit fails for an unsatisfied circuit. */
+ * PLK_E_DEGREE exactly where the reference's commit fails for an unsatisfied circuit, and
+ * with PLK_E_ARG when the circuit's structure (gates, wires, selectors, public-input
+ * positions) differs from the one the key was compiled from or its witness vector is too
+ * short for the key's wires. */
 int plk_prove(plk_key* key, const plk_composer* circuit, uint64_t seed, plk_proof* proof,
               plk_fr* public_inputs, size_t pi_cap, size_t* pi_count);
+
+/* ---- prover lanes: several proofs in flight over one key ----------------------------
+ * Prover: Clone + create_proof(&self) may run concurrently in the reference.
+ * A plk_prover is one such concurrent prover: its own HIP stream, MSM workspace, NTT
+ * scratch and per-proof buffers, sharing the key's device-resident tables and the SRS
+ * window table read-only (one copy per GPU however many proofs are in flight). Provers of
+ * one key may run plk_prover_prove from different threads at the same time. Destroy every
+ * prover of a key before the key. plk_prove(key, ...) is plk_prover_prove on a default
+ * prover the key owns (on the context's stream). */
+typedef struct plk_prover plk_prover;
+int plk_prover_create(plk_key* key, plk_prover** out);
+int plk_prover_destroy(plk_prover* p);
+/* The prover's stream (hipStream_t). */
+int plk_prover_stream(plk_prover* p, void** stream_out);
+/* Prover::create_proof (prover.rs:67-474) on this prover; arguments as plk_prove. */
+int plk_prover_prove(plk_prover* p, const plk_composer* circuit, uint64_t seed, plk_proof* proof,
+                     plk_fr* public_inputs, size_t pi_cap, size_t* pi_count);
+/* k_accumulate statistics of this prover's MSMs (see plk_srs_cum_msm_stats); reset != 0
+ * clears the cumulative figures after reading them. Any output may be NULL. */
+int plk_prover_msm_stats(plk_prover* p, int reset, double* accumulate_ms, uint64_t* launches,
+                         uint64_t* point_adds, uint64_t* points);
+
+/* ---- sharded commits: one proof, its MSMs split over the GPUs of a node ------------------
+ * BASELINE configs[4] / SURVEY §8e. One process (rank) per GPU proves the SAME circuit with
+ * the same seed; every rank runs the NTT / elementwise rounds on its own GPU (replicas, they
+ * are a minority of the proof) and each commit — the 4 wire commits (prover.rs:133-136),
+ * z (:194), the 4 quotient chunks (:262-265) and the 2 openings (:440,452) — is split by
+ * SRS index: rank r runs the Pippenger over its slice [slice_start, slice_start +
+ * slice_len) of every polynomial against `slice` (plk_srs_setup_range on the same tau), then
+ * the ranks exchange their partial points (13 words + a status word per commit) with ONE
+ * all-gather per commit group and each folds them on the host (plk_g1_sum order: rank 0
+ * first). Proofs are byte-identical to the unsharded plk_prove on any rank.
+ * The all-gather is the caller's (RCCL over xGMI under torch.distributed in
+ * dusk-plonk_amd/parallel.py): `allgather(user, send, bytes, recv)` must place every rank's
+ * `bytes` of `send` at recv + rank * bytes and return 0 (non-zero: PLK_E_DEVICE). Slices
+ * must tile [0, N) in rank order with N >= the key's trimmed SRS; every rank calls
+ * plk_prover_prove for every proof, in the same order (the exchange is a collective). */
+typedef int (*plk_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
+int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int rank, int world,
+                     plk_allgather_fn allgather, void* user);
+
+/* ---- Proof wire format (SCALE, src/prover/proof.rs:11,36) ---------------------------------
+ * The reference derives parity-scale-codec Encode/Decode for Proof: fields in declaration
+ * order, 11 Commitment<G1Affine> then ProofEvaluations. The element encodings live in the
+ * un-vendored bls-12-381 / zksnarks crates; ASSUMED here (parity unpinned): G1Affine as its
+ * fields x, y (Fq = [u64; 6] Montgomery limbs, LE) and is_infinity (bool, 1 byte) = 97 B;
+ * Fr as [u64; 4] Montgomery limbs, LE = 32 B; ProofEvaluations in plk_proof order. Total
+ * PLK_PROOF_SCALE_BYTES. Decode rejects (PLK_E_ARG) a wrong length, a non-boolean flag,
+ * limbs >= the modulus, and points not on y^2 = x^3 + 4. */
+#define PLK_PROOF_SCALE_BYTES (11 * 97 + 16 * 32)
+int plk_proof_encode(const plk_proof* proof, uint8_t* out, size_t cap, size_t* len);
+int plk_proof_decode(const uint8_t* in, size_t len, plk_proof* proof);
 
 /* ---- test support ---------------------------------------------------------------- */
 /* Elementwise device field arithmetic on host arrays (used by the parity tests to pin the

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(plk):
 
 def test_version_and_status_strings(plk):
     lib = plk.plonk._lib()
-    assert lib.plk_abi_version() == 1
+    assert lib.plk_abi_version() == 2  # 2: plk_prover lanes, sharded commits, SCALE codec
     assert b"degree" in lib.plk_status_str(plk.PLK_E_DEGREE)
     assert lib.plk_status_str(99) == b"unknown status"
 
@@ -39,6 +39,12 @@ def test_null_arguments_are_rejected_without_gpu(plk):
     assert lib.plk_commit(None, None, 0, None) == plk.PLK_E_ARG
     assert lib.plk_srs_len(None, None) == plk.PLK_E_ARG
     assert lib.plk_msm_sharded(None, 0, None, 0, None) == plk.PLK_E_ARG
+    from dusk_plonk_amd.prover import _bind
+    b = _bind()
+    assert b.plk_prover_create(None, None) == plk.PLK_E_ARG
+    assert b.plk_prover_prove(None, None, 0, None, None, 0, None) == plk.PLK_E_ARG
+    assert b.plk_prover_shard(None, None, 0, 0, 2, None, None) == plk.PLK_E_ARG
+    assert b.plk_proof_decode(None, 0, None) == plk.PLK_E_ARG
 
 
 def test_device_count_never_fails(plk):

@@ -18,7 +18,8 @@ ROOFLINE = ("bound", "achieved", "peak", "unit", "frac", "traffic")
 
 def run_bench(*args, timeout=100):
     env = dict(os.environ)
-    env.pop("WORLD_SIZE", None)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
     p = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stderr[-2000:]
@@ -27,13 +28,13 @@ def run_bench(*args, timeout=100):
     return json.loads(lines[0])
 
 
-def check_contract(d, steps, warmup):
+def check_contract(d, steps, warmup, n_gpus=1):
     for k in CONTRACT:
         assert k in d, k
     for k in ROOFLINE:
         assert k in d["roofline"], k
     assert d["value"] > 0 and d["ms_per_step"] > 0
-    assert d["n_gpus"] == 1 and d["steps"] == steps and d["warmup"] == warmup
+    assert d["n_gpus"] == n_gpus and d["steps"] == steps and d["warmup"] == warmup
     assert d["higher_is_better"] is True and d["vs_baseline"] is None
     assert "workload" in d["config"]
     assert d["roofline"]["frac"] == pytest.approx(d["roofline"]["achieved"] / d["roofline"]["peak"])
@@ -68,4 +69,37 @@ def test_prove_mode_line():
     check_contract(d, 2, 1)
     assert d["unit"] == "constraints/s" and d["scaling"] == "weak"
     # value counts every lane's proof: n * steps * lanes / time
+    assert d["value"] == pytest.approx(4096 * 2 * 2 / (d["ms_per_step"] * 2e-3), rel=1e-6)
+
+
+def test_gpus_flag_must_match_launcher():
+    """Under a launcher (WORLD_SIZE set) --gpus must agree with it: no silent n_gpus: 1."""
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0 and "WORLD_SIZE=3" in (p.stderr + p.stdout)
+
+
+@pytest.mark.gpu
+def test_prove_mode_line_has_solo_roofline():
+    d = run_bench("--log-n", "12", "--steps", "2", "--warmup", "1", "--lanes", "2",
+                  "--no-cpu-baseline")
+    r = d["roofline"]
+    assert r["kernel"] == "k_accumulate" and r["solo"]["launches"] == 4  # one proof
+    assert r["avg_launch_ms"] == r["solo"]["avg_launch_ms"]
+    assert r["in_workload"]["launches"] == 2 * 2 * 4
+    assert "13 transforms" in d["config"]["workload"] and "1 public input" in d["config"]["workload"]
+
+
+@pytest.mark.gpu
+def test_gpus_2_shard_msm_launches_ranks_itself():
+    """`bench.py --gpus 2 --shard-msm` without a launcher starts two ranks (here sharing the
+    box's one GPU over gloo) and prints ONE full-proof line with n_gpus 2 (configs[4] form)."""
+    d = run_bench("--gpus", "2", "--shard-msm", "--dist-backend", "gloo", "--log-n", "12",
+                  "--steps", "2", "--warmup", "1", "--lanes", "2", "--no-cpu-baseline",
+                  timeout=300)
+    check_contract(d, 2, 1, n_gpus=2)
+    assert d["scaling"] == "strong" and d["config"]["proofs_per_step"] == 2
+    assert d["config"]["parallelism"].startswith("msm-shard x2")
+    # all ranks prove the same proofs: value counts each once
     assert d["value"] == pytest.approx(4096 * 2 * 2 / (d["ms_per_step"] * 2e-3), rel=1e-6)

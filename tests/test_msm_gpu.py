@@ -122,6 +122,22 @@ def test_commit_dev_and_stats(plk, gpu_ctx, oracle):
 
 
 @pytest.mark.slow
+def test_msm_2_20_vs_oracle(plk, gpu_ctx, oracle):
+    """BASELINE configs[2] at its full size: a 2^20-point MSM over the bench SRS (c = 16, 16
+    windows of the window table) bit-exact against the C oracle's Pippenger, random and
+    sparse scalars."""
+    import os
+    n = 1 << 20
+    pp = plk.PlonkParams.setup(20, random_fr(1, seed=20)[0], gpu_ctx)
+    pts = pp.points(0, n)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    sc = random_fr(n, seed=23)
+    assert np.array_equal(pp.msm(sc).words, oracle.msm(pts, sc, threads))
+    sparse = np.where((np.arange(n) % 29 == 0)[:, None], sc, 0).astype(np.uint64)
+    assert np.array_equal(pp.msm(sparse).words, oracle.msm(pts, sparse, threads))
+
+
+@pytest.mark.slow
 def test_msm_2_20_properties(plk, gpu_ctx):
     """2^20: linearity commit(a) + commit(b) == commit(a + b), and commit(e_i) == g1[i]."""
     n = 1 << 20

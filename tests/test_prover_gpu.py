@@ -113,8 +113,8 @@ def test_proofs_are_deterministic_per_seed(plk):
     p1, _ = prover.create_proof(99, Chain(40, 5))
     p2, _ = prover.create_proof(99, Chain(40, 5))
     p3, _ = prover.create_proof(100, Chain(40, 5))
-    assert p1.to_bytes() == p2.to_bytes()
-    assert p1.to_bytes() != p3.to_bytes()
+    assert p1.raw_bytes() == p2.raw_bytes()
+    assert p1.raw_bytes() != p3.raw_bytes()
 
 
 @pytest.mark.parametrize("logn", [6, 10, 12, 16, 20])

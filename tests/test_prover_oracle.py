@@ -278,8 +278,41 @@ def test_gpu_proof_equals_oracle(plk, oracle, name, fn, seed):
     proof, pis = prover.prove_composer(cs, seed)
     for i, c in enumerate(COMMS):
         assert np.array_equal(getattr(proof, c), ref["comms"][i]), c
-    raw = np.frombuffer(proof.to_bytes(), dtype=np.uint64)
+    raw = np.frombuffer(proof.raw_bytes(), dtype=np.uint64)
     evals = raw[11 * 13:].reshape(16, 4)
     assert np.array_equal(evals, ref["evals"]), "evaluations differ"
     from dusk_plonk_amd.prover import fr_int
     assert pis == [fr_int(p) for p in ref["pis"]]
+
+
+def bench_chain(chain_gates, seed):
+    """bench.py's circuit (bench_circuit): Plonk::initialize + chain + one public input."""
+    def f(cs):
+        cs.synthetic_chain(chain_gates, seed)
+        cs.append_public((seed * 0x9E3779B97F4A7C15 + 12345) % (1 << 250))
+    return f
+
+
+@pytest.mark.gpu
+def test_gpu_proof_equals_oracle_bench_2_16(plk, oracle):
+    """BASELINE configs[3] at its full size: the bench circuit at n = 2^16 (m = n - 8 gates,
+    one public input, so the PI idft / coset_dft run), GPU proof byte for byte against the
+    restated CPU prover on the same SRS, label and blinding seed."""
+    import os
+    from dusk_plonk_amd.prover import PlonkKey, fr_int
+    k = 16
+    tau_limbs, _ = tau_for(0x5EED)
+    cs = build(bench_chain((1 << k) - 15, 77))
+    gates, wit = cs.export()
+    assert gates.shape[0] == (1 << k) - 8
+    pp = plk.PlonkParams.setup(k, tau_limbs)
+    srs = pp.points(0, n_trim(gates.shape[0]))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    ref = oracle.prove(gates, wit, srs, b"bench", 7, threads)
+    prover, vd = PlonkKey.compile_composer(pp, b"bench", cs)
+    assert np.array_equal(vd.comms, ref["vk"])
+    proof, pis = prover.prove_composer(cs, 7)
+    raw = np.frombuffer(proof.raw_bytes(), dtype=np.uint64)
+    assert np.array_equal(raw[: 11 * 13].reshape(11, 13), ref["comms"])
+    assert np.array_equal(raw[11 * 13:].reshape(16, 4), ref["evals"])
+    assert len(pis) == 1 and pis == [fr_int(p) for p in ref["pis"]]
