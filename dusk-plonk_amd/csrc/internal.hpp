@@ -198,6 +198,22 @@ struct DeviceGuard {
 };
 
 int ntt_build_domain(plk_domain* d);
+// Per-launch strides of a batch of `count` transforms (vector v: in + v * in_stride, out + v *
+// out_stride, pre-scale table pre + v * pre_stride, post-scale table post + v * post_stride;
+// a stride of 0 shares one input / table between the vectors). pre / post: R'-domain tables
+// replacing the domain's g^j (forward coset) / n^-1 g^-j (inverse coset) tables.
+struct NttBatch {
+  uint64_t in_stride = 0, out_stride = 0;
+  const Fr* pre = nullptr;
+  uint64_t pre_stride = 0;
+  const Fr* post = nullptr;
+  uint64_t post_stride = 0;
+};
+struct NttStrides {  // kernel-side view
+  uint64_t in, out, pre, post;
+};
+int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset,
+                  Fr* scratch, hipStream_t stream, uint32_t count, const NttBatch& b);
 // pre_table (forward coset transforms only): R'-domain multipliers for the len_in inputs
 // in place of the domain's g^j table — a scaled table (c g^j) yields the evaluations of c p
 int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset,
@@ -216,5 +232,8 @@ const MsmStats& msm_workspace_stats(const MsmWorkspace& w);
 MsmStats& msm_workspace_stats(MsmWorkspace& w);
 void fr_root_of_unity(uint32_t log_n, Fr& omega);
 int ntt_vanishing(plk_domain* d, uint64_t deg, Fr* d_out, hipStream_t s);
+// out[e] = base^e * scale, e < n (R domain; to_rx: converted to the R' domain)
+int ntt_power_table(Fr* out, const Fr& base, const Fr& scale, uint64_t n, bool to_rx,
+                    hipStream_t s);
 int srs_generate(plk_srs* s, const Fr& tau_mont, uint64_t start, hipStream_t stream);
 }  // namespace plk

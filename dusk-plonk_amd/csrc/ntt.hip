@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
                                                   const Fr* __restrict__ pre,
                                                   const Fr* __restrict__ post, Fr post_scalar,
                                                   uint32_t log_n, uint32_t lp, uint32_t lr,
-                                                  uint32_t lt, uint64_t len_in, uint64_t n_stride) {
+                                                  uint32_t lt, uint64_t len_in, NttStrides str) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem32[];
   const uint32_t R = 1u << lr, T = 1u << lt, p = 1u << lp;
   const uint32_t E = R << lt, H = R >> 1;
@@ -96,9 +96,11 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   uint32_t* data = smem32;          // kL planes of E
   uint32_t* twl = smem32 + kL * E;
 
-  const size_t voff = (size_t)blockIdx.y * n_stride;
-  in += voff;
-  out += voff;
+  // vector blockIdx.y of a batch: its input, output and scale-table rows
+  in += (size_t)blockIdx.y * str.in;
+  out += (size_t)blockIdx.y * str.out;
+  if (PRE == 1) pre += (size_t)blockIdx.y * str.pre;
+  if (POST == 2) post += (size_t)blockIdx.y * str.post;
 
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   const uint32_t nr_log = log_n - lr;  // log2(N/R)
@@ -353,14 +355,26 @@ int ntt_build_domain(plk_domain* d) {
 
 int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset, Fr* scratch,
             hipStream_t stream, uint32_t count, const Fr* pre_table) {
+  NttBatch b;
+  b.in_stride = b.out_stride = d->n;
+  b.pre = pre_table;
+  return ntt_run_batch(d, in, out, len_in, dir, coset, scratch, stream, count, b);
+}
+
+int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset,
+                  Fr* scratch, hipStream_t stream, uint32_t count, const NttBatch& bt) {
   const uint64_t n = d->n;
-  if (len_in > n) return PLK_E_ARG;
-  if (n == 1) {  // size-1 transform: identity (times n^-1 = 1, g^0 = 1)
+  if (len_in > n || count == 0) return PLK_E_ARG;
+  const Fr* pre_table = bt.pre;
+  if (n == 1) {  // size-1 transform: x * pre[0] (forward coset) or x * post[0]; else identity
+    if (bt.pre || bt.post) return PLK_E_ARG;  // not needed by any caller
     for (uint32_t v = 0; v < count; ++v) {
+      Fr* o = out + v * bt.out_stride;
+      const Fr* i = in + v * bt.in_stride;
       if (len_in == 0) {
-        PLK_HIP_TRY(hipMemsetAsync(out + v, 0, sizeof(Fr), stream));
-      } else if (in != out) {
-        PLK_HIP_TRY(hipMemcpyAsync(out + v, in + v, sizeof(Fr), hipMemcpyDeviceToDevice, stream));
+        PLK_HIP_TRY(hipMemsetAsync(o, 0, sizeof(Fr), stream));
+      } else if (i != o) {
+        PLK_HIP_TRY(hipMemcpyAsync(o, i, sizeof(Fr), hipMemcpyDeviceToDevice, stream));
       }
     }
     return PLK_OK;
@@ -395,11 +409,16 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
     dim3 grid(blocks, count);
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
+    NttStrides str;
+    str.in = first ? bt.in_stride : n * 1;
+    str.out = last ? bt.out_stride : n * 1;
+    str.pre = bt.pre ? bt.pre_stride : 0;
+    str.post = bt.post ? bt.post_stride : 0;
 #define PLK_LAUNCH(PRE, POST, PRUNE)                                                    \
   hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE>), grid, dim3(bd), lds, stream, src, dst, tw, ptw, \
-                     pre_table ? pre_table : d->coset_pow.as<Fr>(), d->icoset_scale.as<Fr>(), \
-                     n_inv_rx, d->log_n,                                                      \
-                     ps.lp, ps.lr, ps.lt, lin, (uint64_t)n)
+                     pre_table ? pre_table : d->coset_pow.as<Fr>(),                    \
+                     bt.post ? bt.post : d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n, \
+                     ps.lp, ps.lr, ps.lt, lin, str)
     if (prune) {
       if (pre == 1) PLK_LAUNCH(1, 0, 1);
       else PLK_LAUNCH(0, 0, 1);
@@ -413,6 +432,16 @@ int ntt_run(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int co
     PLK_HIP_TRY(hipGetLastError());
     src = dst;
   }
+  return PLK_OK;
+}
+
+int ntt_power_table(Fr* out, const Fr& base, const Fr& scale, uint64_t n, bool to_rx,
+                    hipStream_t s) {
+  if (n == 0) return PLK_OK;
+  const uint32_t nb = (uint32_t)((n + 255) / 256);
+  hipLaunchKernelGGL(k_power_table, dim3(nb), dim3(256), 0, s, out, base, scale, n);
+  if (to_rx) hipLaunchKernelGGL(k_table_to_rx, dim3(nb), dim3(256), 0, s, out, out, n);
+  PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
 }
 

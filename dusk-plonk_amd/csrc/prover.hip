@@ -304,8 +304,9 @@ uint32_t log2_ceil(uint64_t x) {
 // non-zero part is longer than the trimmed SRS fails with PLK_E_DEGREE. `ws` / `s`: the
 // calling prover's MSM workspace and stream.
 int key_commit(plk_key* key, MsmWorkspace& ws, const std::vector<const Fr*>& ptrs,
-               const std::vector<size_t>& lens, plk_g1* outs, int* statuses, hipStream_t s) {
-  const size_t max_points = std::min<size_t>(key->srs->n, key->n_trim);
+               const std::vector<size_t>& lens, plk_g1* outs, int* statuses, hipStream_t s,
+               size_t cap = SIZE_MAX) {
+  const size_t max_points = std::min<size_t>(std::min<size_t>(key->srs->n, key->n_trim), cap);
   std::vector<size_t> use(lens.size());
   for (size_t i = 0; i < lens.size(); ++i) use[i] = std::min(lens[i], max_points);
   int overall = PLK_OK;
@@ -327,10 +328,10 @@ int key_commit(plk_key* key, MsmWorkspace& ws, const std::vector<const Fr*>& ptr
 // takes part in the exchange even when its own MSMs failed, so no rank waits forever on a
 // collective the others left.
 int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
-                 const std::vector<size_t>& lens, plk_g1* outs, int* statuses) {
+                 const std::vector<size_t>& lens, plk_g1* outs, int* statuses, size_t cap) {
   plk_key* key = P->key;
   const size_t cnt = ptrs.size();
-  const size_t max_points = std::min<size_t>(key->srs->n, key->n_trim);
+  const size_t max_points = std::min<size_t>(std::min<size_t>(key->srs->n, key->n_trim), cap);
   const uint64_t lo = P->shard_lo, hi = lo + P->shard->n;
   const bool last = P->rank == P->world - 1;
   std::vector<const Fr*> lp(cnt);
@@ -388,10 +389,23 @@ int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
   return overall;
 }
 
+// cap: commit at most `cap` points, the rest of each polynomial must be zero (else
+// PLK_E_DEGREE) — the quotient chunks' bound below
 int prover_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
-                  const std::vector<size_t>& lens, plk_g1* outs, int* statuses) {
-  if (P->world > 1) return shard_commit(P, ptrs, lens, outs, statuses);
-  return key_commit(P->key, *P->ws, ptrs, lens, outs, statuses, P->stream);
+                  const std::vector<size_t>& lens, plk_g1* outs, int* statuses,
+                  size_t cap = SIZE_MAX) {
+  if (P->world > 1) return shard_commit(P, ptrs, lens, outs, statuses, cap);
+  return key_commit(P->key, *P->ws, ptrs, lens, outs, statuses, P->stream, cap);
+}
+
+// a primitive cube root of unity in Fr: 7^((r-1)/3) = 0xac45a4010001a40200000000ffffffff
+// (Montgomery form)
+Fr cube_root_of_unity() {
+  static const uint32_t w[8] = {0xffffffffu, 0x00000000u, 0x0001a402u, 0xac45a401u,
+                                0u, 0u, 0u, 0u};
+  Fr x;
+  for (int i = 0; i < 8; ++i) x.v[i] = w[i];
+  return fe_to_mont(x);
 }
 
 // JubJub twisted-Edwards d = -10240/10241 mod r
@@ -727,7 +741,7 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     // keypair.trim(additional_n) with additional_n = next_pow2(m + 6) (key.rs:81-82); the
     // trimmed SRS keeps PlonkParams' slack of 8 points
     key->n_trim = (1ull << log2_ceil(m + 6)) + 8;
-    if (k + 3 > 27) return PLK_E_ARG;
+    if (k + 1 > 27) return PLK_E_ARG;
     for (uint64_t i = 0; i < m; ++i) {
       const Gate g = gate_unpack(cs, i);
       if (!fe_is_zero(g.q[QRANGE])) key->has_range = true;
@@ -736,8 +750,8 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
       if (!fe_is_zero(g.q[QVAR])) key->has_var = true;
     }
     TRY(plk_domain_get(ctx, k, &key->dom));
-    TRY(plk_domain_get(ctx, k + 3, &key->dom8));
-    const uint64_t n8 = 8 * n;
+    TRY(plk_domain_get(ctx, k + 1, &key->domq));
+    const uint64_t n2 = 2 * n, nq = kQBlocks * n2;
 
     // 1. selectors padded to n (key.rs:89-119) -> idft (key.rs:121-131)
     std::vector<Fr> host(11 * n, fe_zero<FrCfg>());
@@ -795,42 +809,68 @@ int plk_key_compile(plk_srs* srs, const plk_composer* cs, const char* label, plk
     for (int i = 11; i < 15; ++i)
       if (sts[i] != PLK_OK) return sts[i];
 
-    // 4. 8n coset evaluations (key.rs:220-245) and v_h over the coset (key.rs:291)
-    TRY(key->sel8.alloc(SEL_COUNT8 * n8 * sizeof(Fr)));
-    const int sel_src[SEL_COUNT8] = {QM, QL, QR, QO, Q4, QC, QARITH, QRANGE, QLOGIC, QFIXED, QVAR};
-    const bool sel_used[SEL_COUNT8] = {true, true, true, true, true, true, true, key->has_range,
+    // 4. quotient-domain evaluations (key.rs:220-245 over g H_8n there; g H_6n here, see
+    // prover.hpp) and v_h over it (key.rs:291)
+    {
+      const Fr gq = key->domq->g, one = fe_one<FrCfg>();
+      const Fr w3 = cube_root_of_unity();
+      const uint64_t rowc = n + 8;  // coset table row: the transforms read <= n + 3 inputs
+      TRY(key->coset_s.alloc(kQBlocks * rowc * sizeof(Fr)));
+      TRY(key->coset_w.alloc(kQBlocks * rowc * sizeof(Fr)));
+      TRY(key->coset_pi.alloc(kQBlocks * rowc * sizeof(Fr)));
+      TRY(key->icoset_q.alloc(kQBlocks * n2 * sizeof(Fr)));
+      const Fr c32 = fr_u64(32), inv3 = fe_inv(fr_u64(3));
+      Fr sm = gq;
+      for (int mb = 0; mb < kQBlocks; ++mb) {
+        key->s_m[mb] = sm;
+        TRY(ntt_power_table(key->coset_s.as<Fr>() + mb * rowc, sm, one, rowc, true, s));
+        TRY(ntt_power_table(key->coset_w.as<Fr>() + mb * rowc, sm, c32, rowc, true, s));
+        TRY(ntt_power_table(key->coset_pi.as<Fr>() + mb * rowc, sm, fe_inv(c32), rowc, true, s));
+        TRY(ntt_power_table(key->icoset_q.as<Fr>() + mb * n2, fe_inv(sm),
+                            fe_mul(key->domq->n_inv, inv3), n2, true, s));
+        sm = fe_mul(sm, w3);
+      }
+      // k_coset3_combine: c[k + 2n l] = g^(-2nl) sum_m eta^(-ml) B'_m[k], eta = w3^(2n)
+      const Fr eta_inv = fe_inv(fe_pow_u64(w3, n2));
+      const Fr eta_inv2 = fe_sqr(eta_inv);
+      const Fr g1 = fe_inv(fe_pow_u64(gq, n2)), g2 = fe_sqr(g1);
+      const Fr cm[6] = {g1, fe_mul(g1, eta_inv), fe_mul(g1, eta_inv2),
+                        g2, fe_mul(g2, eta_inv2), fe_mul(g2, eta_inv)};
+      for (int j = 0; j < 6; ++j) key->comb[j] = fe_to_rx_domain(cm[j]);
+      // v_h(s_m w_2n^u) = g^n w3^(mn) (-1)^u - 1: index 2m + (u & 1)
+      for (int mb = 0; mb < kQBlocks; ++mb) {
+        const Fr x = fe_pow_u64(key->s_m[mb], n);
+        key->vh_inv[2 * mb] = fe_inv(fe_sub(x, one));
+        key->vh_inv[2 * mb + 1] = fe_inv(fe_sub(fe_neg(x), one));
+      }
+    }
+    // forward coset transforms of n-coefficient polys onto the three blocks in one launch
+    auto coset_fwd = [&](const Fr* in, Fr* out, uint64_t len, const DevBuf& table) {
+      NttBatch b;
+      b.in_stride = 0;  // the same coefficients for every block
+      b.out_stride = n2;
+      b.pre = table.as<Fr>();
+      b.pre_stride = n + 8;
+      return ntt_run_batch(key->domq, in, out, len, 1, 1, nullptr, s, kQBlocks, b);
+    };
+    TRY(key->selq.alloc(SEL_COUNTQ * nq * sizeof(Fr)));
+    const int sel_src[SEL_COUNTQ] = {QM, QL, QR, QO, Q4, QC, QARITH, QRANGE, QLOGIC, QFIXED, QVAR};
+    const bool sel_used[SEL_COUNTQ] = {true, true, true, true, true, true, true, key->has_range,
                                        key->has_logic, key->has_fixed, key->has_var};
-    for (int j = 0; j < SEL_COUNT8; ++j)  // unused widget selectors are never read
+    for (int j = 0; j < SEL_COUNTQ; ++j)  // unused widget selectors are never read
       if (sel_used[j])
-        TRY(ntt_run(key->dom8, qc + sel_src[j] * n, key->sel8.as<Fr>() + j * n8, n, 1, 1, nullptr, s, 1));
-    TRY(key->sigma8.alloc(4 * n8 * sizeof(Fr)));
+        TRY(coset_fwd(qc + sel_src[j] * n, key->selq.as<Fr>() + j * nq, n, key->coset_s));
+    TRY(key->sigmaq.alloc(4 * nq * sizeof(Fr)));
     for (int c = 0; c < 4; ++c)
-      TRY(ntt_run(key->dom8, sc + c * n, key->sigma8.as<Fr>() + c * n8, n, 1, 1, nullptr, s, 1));
-    // L1 over the 8n coset, shared by every proof: idft(e_0) = n^-1 in every coefficient
-    TRY(key->l1_8n.alloc(n8 * sizeof(Fr)));
+      TRY(coset_fwd(sc + c * n, key->sigmaq.as<Fr>() + c * nq, n, key->coset_s));
+    // L1 over the quotient domain, shared by every proof: idft(e_0) = n^-1 in every coefficient
+    TRY(key->l1q.alloc(nq * sizeof(Fr)));
     {
       DevBuf tmp;
       TRY(tmp.alloc(n * sizeof(Fr)));
       TRY(pk_fill(tmp.as<Fr>(), key->dom->n_inv, n, s));
-      TRY(ntt_run(key->dom8, tmp.as<Fr>(), key->l1_8n.as<Fr>(), n, 1, 1, nullptr, s, 1));
+      TRY(coset_fwd(tmp.as<Fr>(), key->l1q.as<Fr>(), n, key->coset_s));
       PLK_HIP_TRY(stream_wait(s));
-    }
-    // coset tables with 2^5 / 2^-5 folded in (k_quotient exponents, prover.hpp): the wire
-    // and public-input transforms read at most n + 3 coefficients
-    {
-      const uint64_t nt = std::min<uint64_t>(n8, n + 8);
-      TRY(key->coset_w.alloc(nt * sizeof(Fr)));
-      TRY(key->coset_pi.alloc(nt * sizeof(Fr)));
-      const Fr c32 = fr_u64(32);
-      TRY(pk_scale_copy(key->dom8->coset_pow.as<Fr>(), c32, key->coset_w.as<Fr>(), nt, s));
-      TRY(pk_scale_copy(key->dom8->coset_pow.as<Fr>(), fe_inv(c32), key->coset_pi.as<Fr>(), nt, s));
-    }
-    // v_h[i] = (g w8^i)^n - 1 has period 8: invert the 8 values once
-    const Fr gn = fe_pow_u64(key->dom8->g, n), wn = fe_pow_u64(key->dom8->omega, n);
-    Fr x = gn;
-    for (int j = 0; j < 8; ++j) {
-      key->vh_inv[j] = fe_inv(fe_sub(x, fe_one<FrCfg>()));
-      x = fe_mul(x, wn);
     }
     // 5. wire indices for the per-proof gather (prover.rs:114-119)
     std::vector<uint32_t> idx(4 * n, 0);
@@ -959,7 +999,8 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     if (cs->witness.size() <= key->max_wire) return PLK_E_ARG;
     DeviceGuard guard(key->ctx->device);
     hipStream_t s = P->stream;
-    const uint64_t n = key->n, m = key->m, n8 = 8 * n, S = n + 8;  // S: padded poly stride
+    const uint64_t n = key->n, m = key->m, S = n + 8;  // S: padded poly stride
+    const uint64_t n2 = 2 * n, nq = kQBlocks * n2;       // quotient domain (prover.hpp)
     Rng rng{seed};
     const Fr one = fe_one<FrCfg>();
     const Fr K1 = fr_u64(7), K2 = fr_u64(13), K3 = fr_u64(17);
@@ -975,17 +1016,17 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     TRY(P->scan_tmp.alloc((pk_scan_tmp_elems(5 * n) + 1) * sizeof(Fr)));
     TRY(P->pi_lag.alloc(n * sizeof(Fr)));
     TRY(P->pi_coef.alloc(n * sizeof(Fr)));
-    TRY(P->ev8.alloc(6 * n8 * sizeof(Fr)));
-    TRY(P->quot8.alloc(n8 * sizeof(Fr)));
-    TRY(P->t_coef.alloc(n8 * sizeof(Fr)));
+    TRY(P->evq.alloc(6 * nq * sizeof(Fr)));
+    TRY(P->quotq.alloc(nq * sizeof(Fr)));
+    TRY(P->t_coef.alloc(nq * sizeof(Fr)));
     TRY(P->r_coef.alloc(S * sizeof(Fr)));
     TRY(P->agg.alloc(5 * n * sizeof(Fr)));
     TRY(P->agg2.alloc(S * sizeof(Fr)));
     TRY(P->w_coef.alloc((5 * n + S) * sizeof(Fr)));
     TRY(P->tmp_a.alloc(5 * n * sizeof(Fr)));
-    TRY(P->eval_partial.alloc((size_t)kMaxEval * pk_eval_max_blocks(n8) * sizeof(Fr)));
+    TRY(P->eval_partial.alloc((size_t)kMaxEval * pk_eval_max_blocks(nq) * sizeof(Fr)));
     TRY(P->eval_out.alloc(kMaxEval * sizeof(Fr)));
-    TRY(P->ntt_scratch.alloc(2 * n8 * sizeof(Fr)));
+    TRY(P->ntt_scratch.alloc(2 * nq * sizeof(Fr)));
     Fr* nsc = P->ntt_scratch.as<Fr>();
 
     // transcript seeded like Prover::new (prover.rs:54-55): Transcript::base(label, vk, m)
@@ -1084,34 +1125,41 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
       PLK_HIP_TRY(hipMemcpyAsync(pil + pis[i].first, P->pin_small.as<Fr>() + i, sizeof(Fr),
                                  hipMemcpyHostToDevice, s));
     }
-    Fr* ev = P->ev8.as<Fr>();  // z, a, b, c, d, pi over the 8n coset
+    // the six polynomials over the quotient domain (quotient_poly.rs:54-58,145 over g H_8n
+    // there): each a batch of the three coset blocks (prover.hpp) in one launch per pass
+    Fr* ev = P->evq.as<Fr>();  // z, a, b, c, d, pi, nq points each
+    auto coset_fwd = [&](const Fr* in, Fr* out, uint64_t len, const DevBuf& table) {
+      NttBatch b;
+      b.in_stride = 0;
+      b.out_stride = n2;
+      b.pre = table.as<Fr>();
+      b.pre_stride = n + 8;
+      return ntt_run_batch(key->domq, in, out, len, 1, 1, nsc, s, kQBlocks, b);
+    };
     if (!pis.empty()) TRY(ntt_run(key->dom, pil, P->pi_coef.as<Fr>(), n, -1, 0, nsc, s, 1));
-    TRY(ntt_run(key->dom8, zc, ev + 0 * n8, n + 3, 1, 1, nsc, s, 1));
+    TRY(coset_fwd(zc, ev + 0 * nq, n + 3, key->coset_s));
     // wire evaluations at exponent -1 and PI at +1 for k_quotient's redundant-form
     // arithmetic (QuotientArgs): scaled coset tables, no extra pass
-    for (int c = 0; c < 4; ++c)
-      TRY(ntt_run(key->dom8, wc + c * S, ev + (1 + c) * n8, n + 2, 1, 1, nsc, s, 1,
-                  key->coset_w.as<Fr>()));
+    for (int c = 0; c < 4; ++c) TRY(coset_fwd(wc + c * S, ev + (1 + c) * nq, n + 2, key->coset_w));
     // PI(X) over the coset; a circuit without public inputs has PI = 0 (the term is skipped)
-    if (!pis.empty())
-      TRY(ntt_run(key->dom8, P->pi_coef.as<Fr>(), ev + 5 * n8, n, 1, 1, nsc, s, 1,
-                  key->coset_pi.as<Fr>()));
+    if (!pis.empty()) TRY(coset_fwd(P->pi_coef.as<Fr>(), ev + 5 * nq, n, key->coset_pi));
     const Fr alpha2 = fe_sqr(alpha);
     QuotientArgs qa{};
     qa.z = ev;
-    qa.a = ev + n8;
-    qa.b = ev + 2 * n8;
-    qa.c = ev + 3 * n8;
-    qa.d = ev + 4 * n8;
-    qa.pi = pis.empty() ? nullptr : ev + 5 * n8;
-    qa.l1 = key->l1_8n.as<Fr>();
+    qa.a = ev + nq;
+    qa.b = ev + 2 * nq;
+    qa.c = ev + 3 * nq;
+    qa.d = ev + 4 * nq;
+    qa.pi = pis.empty() ? nullptr : ev + 5 * nq;
+    qa.l1 = key->l1q.as<Fr>();
     qa.alpha2 = alpha2;
-    qa.sel = key->sel8.as<Fr>();
-    qa.sigma = key->sigma8.as<Fr>();
-    qa.elements8 = key->dom8->tw_fwd.as<Fr>();
-    qa.out = P->quot8.as<Fr>();
-    qa.n8 = n8;
-    qa.g = key->dom8->g;
+    qa.sel = key->selq.as<Fr>();
+    qa.sigma = key->sigmaq.as<Fr>();
+    qa.elements = key->domq->tw_fwd.as<Fr>();
+    qa.out = P->quotq.as<Fr>();
+    qa.nq = nq;
+    qa.log_blk = key->k + 1;
+    qa.g = key->domq->g;
     qa.alpha = alpha;
     qa.beta = beta;
     qa.gamma = gamma;
@@ -1139,12 +1187,12 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     qa.edwards_d = edwards_d();
     qa.has_fixed = key->has_fixed ? 1 : 0;
     qa.has_var = key->has_var ? 1 : 0;
-    for (int j = 0; j < 8; ++j) qa.vh_inv[j] = key->vh_inv[j];
+    for (int j = 0; j < 2 * kQBlocks; ++j) qa.vh_inv[j] = key->vh_inv[j];
     {  // exponent-scaled constants for k_quotient (x[e] = x R 2^(-5e); [-1] = R' domain)
       auto em1 = [](const Fr& x) { return fe_to_rx_domain(x); };
       auto em2 = [](const Fr& x) { return fe_to_rx_domain(fe_to_rx_domain(x)); };
       const Fr one = fe_one<FrCfg>(), two = fe_dbl(one);
-      qa.rx_bg = em2(fe_mul(beta, key->dom8->g));
+      for (int mb = 0; mb < kQBlocks; ++mb) qa.rx_bg[mb] = em2(fe_mul(beta, key->s_m[mb]));
       qa.rx_beta = em2(beta);
       qa.rx_gamma = em1(gamma);
       qa.rx_one_w = em1(one);
@@ -1154,20 +1202,37 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
       qa.rx_kappa2 = em1(qa.kappa2);
       qa.rx_kappa3 = em1(qa.kappa3);
       qa.rx_alpha2 = em1(alpha2);
-      for (int j = 0; j < 8; ++j) qa.rx_vh[j] = em2(key->vh_inv[j]);
+      for (int j = 0; j < 2 * kQBlocks; ++j) qa.rx_vh[j] = em2(key->vh_inv[j]);
       qa.rx_32 = fr_u64(32);
       qa.rx_inv32 = fe_inv(qa.rx_32);
     }
     TRY(pk_quotient(qa, s));
     Fr* tc = P->t_coef.as<Fr>();
-    TRY(ntt_run(key->dom8, P->quot8.as<Fr>(), tc, n8, -1, 1, nsc, s, 1));
+    {  // t = coset_idft over the quotient domain (quotient_poly.rs:115): the three blocks'
+       // inverse transforms (post-scaled by (2n)^-1 3^-1 s_m^-k) in place, then the radix-3
+       // combine into the 6n coefficients (t has at most 4n + 7; the rest are zero)
+      NttBatch b;
+      b.in_stride = b.out_stride = n2;
+      b.post = key->icoset_q.as<Fr>();
+      b.post_stride = n2;
+      TRY(ntt_run_batch(key->domq, P->quotq.as<Fr>(), P->quotq.as<Fr>(), n2, -1, 1, nsc, s,
+                        kQBlocks, b));
+      TRY(pk_coset3_combine(P->quotq.as<Fr>(), n2, key->comb, tc, s));
+    }
     // split into t_low, t_mid, t_high (n each) and t_4 = t[3n..] (prover.rs:252-265)
     plk_g1 tcom[4];
-    TRY(prover_commit(P, {tc, tc + n, tc + 2 * n, tc + 3 * n}, {n, n, n, 5 * n}, tcom, nullptr));
-    // t_4 is 5n coefficients in the reference (prover.rs:259); its commit succeeded, so
-    // everything past the committed SRS prefix is zero (the commit checks the tail): t and
-    // t_4 end at 3n + t4_len for the evaluation and the opening below
-    const uint64_t t4_len = std::min<uint64_t>(5 * n, std::min<uint64_t>(key->srs->n, key->n_trim));
+    // t_4 is t[3n..8n) in the reference (prover.rs:259) and t[3n..6n) here. For a satisfied
+    // circuit t has degree <= 4n + 6 on either domain (prover.hpp), so t_4 ends below n + 8:
+    // committing at most n + 8 points changes no commitment, and the zero check of the rest
+    // fails for an unsatisfied circuit (its interpolant does not vanish there) where the
+    // reference's commit fails (t_4 past the trimmed SRS, prover.rs:262-265) — including
+    // tiny circuits whose trimmed SRS covers all of t[3n..6n)
+    TRY(prover_commit(P, {tc, tc + n, tc + 2 * n, tc + 3 * n}, {n, n, n, nq - 3 * n}, tcom,
+                      nullptr, n + 8));
+    // its commit succeeded, so everything past the committed prefix is zero: t and t_4 end at
+    // 3n + t4_len for the evaluation and the opening below
+    const uint64_t t4_len = std::min<uint64_t>(
+        n + 8, std::min<uint64_t>(key->srs->n, key->n_trim));
     tr.append_commitment("t_low", tcom[0]);
     tr.append_commitment("t_mid", tcom[1]);
     tr.append_commitment("t_high", tcom[2]);

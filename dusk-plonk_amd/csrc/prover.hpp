@@ -16,14 +16,26 @@ struct BlindArgs {
   uint32_t count;
 };
 
-// selector rows of the 8n evaluation table
+// selector rows of the quotient-domain evaluation table
 enum { SEL_QM = 0, SEL_QL, SEL_QR, SEL_QO, SEL_Q4, SEL_QC, SEL_QARITH, SEL_QRANGE, SEL_QLOGIC,
-       SEL_QFIXED, SEL_QVAR, SEL_COUNT8 };
+       SEL_QFIXED, SEL_QVAR, SEL_COUNTQ };
+
+// The quotient domain (round 3). The reference evaluates the quotient over the coset g H_8n
+// (quotient_poly.rs:52-58,115); the numerator has degree at most 5n + 6 (z times four wire
+// factors) and t = num / Z_H at most 4n + 6, so any coset of more than 5n + 6 points
+// interpolates the same t — bit-identical coefficients, commitments and proofs. This backend
+// uses 6n points: g w3^m H_2n for m < 3 (w3 a primitive cube root of unity; gcd(3, 2n) = 1, so
+// the three cosets form g H_6n), 25% fewer points than 8n. Every quotient-domain vector is
+// laid out in three blocks of 2n (block m = coset m, natural order in u): evaluation point
+// x(m, u) = s_m w_2n^u with s_m = g w3^m, the next row (w_n x) is u + 2 in the same block, and
+// v_h(x) = x^n - 1 = g^n w3^(mn) (-1)^u - 1 takes 6 values (index 2m + (u & 1)).
+constexpr int kQBlocks = 3;
 
 struct QuotientArgs {
-  const Fr *a, *b, *c, *d, *z, *pi, *l1, *sel, *sigma, *elements8;  // pi null: no public inputs
+  const Fr *a, *b, *c, *d, *z, *pi, *l1, *sel, *sigma, *elements;  // pi null: no public inputs
   Fr* out;
-  uint64_t n8;
+  uint64_t nq;        // quotient-domain points (6n): kQBlocks blocks of 2n
+  uint32_t log_blk;   // log2(2n)
   Fr g, alpha, alpha2, beta, gamma, k1, k2, k3;
   Fr range_sep, kappa, kappa2, kappa3;
   Fr logic_sep, lk, lk2, lk3, lk4;  // logic separation challenge and its kappa powers
@@ -31,17 +43,17 @@ struct QuotientArgs {
   Fr var_sep, vk, vk2;               // variable-base addition: sep, kappa = sep^2, ^2
   Fr edwards_d;                      // JubJub d = -10240/10241
   int has_range, has_logic, has_fixed, has_var;
-  Fr vh_inv[8];
+  Fr vh_inv[2 * kQBlocks];  // 1 / v_h, index 2m + (u & 1)
   // k_quotient runs in the redundant form (ffr.hpp): a value with exponent e is stored as
   // x R 2^(-5e) (e = 0: the R domain; e = -1: the R' domain) and rx_mul adds exponents
   // plus one. Wire evaluations arrive at e = -1 (coset table scaled by 2^5), public
   // inputs at e = +1, z / selectors / sigmas / L1 / elements at e = 0; these constants are
   // pre-scaled so every term meets at e = 1 and num / v_h lands at e = 0 (the R domain).
-  Fr rx_bg, rx_beta, rx_gamma;          // beta g and beta at e = -2, gamma at e = -1
+  Fr rx_bg[kQBlocks], rx_beta, rx_gamma;  // beta s_m and beta at e = -2, gamma at e = -1
   Fr rx_one_w, rx_two_w, rx_three_w;    // 1, 2, 3 at e = -1 (range widget deltas)
   Fr rx_kappa, rx_kappa2, rx_kappa3;    // range kappa powers at e = -1
   Fr rx_alpha2;                         // alpha^2 at e = -1 (alpha and range_sep at e = 0)
-  Fr rx_vh[8];                          // 1 / v_h at e = -2
+  Fr rx_vh[2 * kQBlocks];               // 1 / v_h at e = -2
   Fr rx_inv32, rx_32;                   // 2^-5 and 2^5 (R domain): k_quotient_ext converts
 };
 
@@ -135,6 +147,10 @@ uint64_t pk_scan_tmp_elems(uint64_t n);
 int pk_scan(const Fr* in, Fr* out, uint64_t n, bool mul, bool suffix, bool exclusive, Fr* tmp,
             hipStream_t s);
 int pk_quotient(const QuotientArgs& q, hipStream_t s);
+// t coefficients from the kQBlocks inverse block transforms B'_m (scaled by (2n)^-1 3^-1 s_m^-k):
+// out[k + 2n l] = g^(-2nl) sum_m eta^(-ml) B'_m[k], eta = w3^(2n); comb = R'-domain constants
+// {g^-2n, g^-2n eta^-1, g^-2n eta^-2, g^-4n, g^-4n eta^-2, g^-4n eta^-1}
+int pk_coset3_combine(const Fr* in, uint64_t n2, const Fr* comb, Fr* out, hipStream_t s);
 // out[j] = in[j] * c (packed Montgomery product), j < n
 int pk_scale_copy(const Fr* in, const Fr& c, Fr* out, uint64_t n, hipStream_t s);
 uint32_t pk_eval_max_blocks(uint64_t max_len);
@@ -193,19 +209,23 @@ struct plk_key {
   uint64_t m = 0, n = 0, n_trim = 0;
   uint32_t k = 0;
   plk_domain* dom = nullptr;   // n
-  plk_domain* dom8 = nullptr;  // 8n
+  plk_domain* domq = nullptr;  // 2n: the blocks of the 6n quotient domain (prover.hpp top)
   bool has_range = false, has_logic = false, has_fixed = false, has_var = false;
   // device-resident proving key
   plk::DevBuf q_coef;       // 11 x n selector coefficient polys
-  plk::DevBuf sel8;         // SEL_COUNT8 x 8n coset evaluations
+  plk::DevBuf selq;         // SEL_COUNTQ x 6n quotient-domain evaluations
   plk::DevBuf sigma_coef;   // 4 x n
   plk::DevBuf sigma_lag;    // 4 x n Lagrange values (= dft of sigma_coef, cached)
-  plk::DevBuf sigma8;       // 4 x 8n
-  plk::DevBuf l1_8n;        // L1 over the 8n coset: coset_dft(idft(e_0)) (quotient_poly.rs:264-272)
-  plk::DevBuf coset_w;      // 2^5 g^j (R' domain), j < n + 8: wire evaluations at e = -1
-  plk::DevBuf coset_pi;     // 2^-5 g^j (R' domain): public-input evaluations at e = +1
+  plk::DevBuf sigmaq;       // 4 x 6n
+  plk::DevBuf l1q;          // L1 over the quotient domain: coset_dft(idft(e_0)) (quotient_poly.rs:264-272)
+  // forward coset tables, kQBlocks rows of n + 8 (R' domain): s_m^j for selectors, sigmas,
+  // L1 and z; 2^5 s_m^j for the wires (evaluations at e = -1); 2^-5 s_m^j for PI (e = +1)
+  plk::DevBuf coset_s, coset_w, coset_pi;
+  plk::DevBuf icoset_q;     // kQBlocks rows of 2n: (2n)^-1 3^-1 s_m^-k (R'), inverse blocks
+  plk::Fr s_m[plk::kQBlocks];    // g w3^m (R domain)
+  plk::Fr comb[6];          // k_coset3_combine constants (R'): g^-2n w3'^-l m, l = 1, 2
   plk::DevBuf wire_idx;     // 4 x n witness indices per gate (u32)
-  plk::Fr vh_inv[8];
+  plk::Fr vh_inv[2 * plk::kQBlocks];
   plk_g1 comms[15];         // q_m q_l q_r q_o q_c q_4 q_arith q_range q_logic q_fixed q_var s1..s4
   // the circuit the key was compiled from: plk_prove refuses a circuit whose structure hash
   // differs or whose witness vector does not cover the largest wire index (prover.rs:114-119
@@ -235,6 +255,6 @@ struct plk_prover {
   // per-proof scratch
   plk::PinnedBuf pin_witness, pin_small;  // host staging of the witness upload / small readbacks
   plk::DevBuf witness, wires_lag, wires_coef, z_lag, z_coef, num, den, tmp_a, scan_tmp, pi_lag,
-      pi_coef, ev8, quot8, t_coef, r_coef, agg, agg2, w_coef, eval_partial, eval_out, ntt_scratch;
+      pi_coef, evq, quotq, t_coef, r_coef, agg, agg2, w_coef, eval_partial, eval_out, ntt_scratch;
   ~plk_prover();
 };

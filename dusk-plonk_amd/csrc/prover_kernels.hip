@@ -226,9 +226,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
   // a value stored as x R 2^(-5e); rx_mul(x[e1], y[e2]) = xy[e1 + e2 + 1]; additions need
   // equal exponents. Wires [-1], z / selectors / sigmas / L1 / elements [0].
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t N = q.n8;
+  const uint64_t N = q.nq;
   if (i >= N) return;
-  const uint64_t nx = (i + 8) & (N - 1);  // "next row" of the n-domain inside the 8n domain
+  // quotient-domain block m (coset g w3^m H_2n), position u; the next row w_n x is u + 2
+  const uint64_t blk = i >> q.log_blk, u = i & ((1ull << q.log_blk) - 1);
+  const uint64_t nx = (blk << q.log_blk) + ((u + 2) & ((1ull << q.log_blk) - 1));
   const RFr a = ldr(&q.a[i]), b = ldr(&q.b[i]), c = ldr(&q.c[i]), d = ldr(&q.d[i]);
   const RFr z = ldr(&q.z[i]), z_next = ldr(&q.z[nx]);
   // arithmetic widget: q_arith (q_m a b + q_l a + q_r b + q_o c + q_4 d + q_c), terms [0]
@@ -264,7 +266,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
   //                    - z_next (a + b s1 + g)(b + b s2 + g)(c + b s3 + g)(d + b s4 + g) ]
   //              + (z - 1) L1(X) alpha^2
   // K1..K3 = 7, 13, 17 (permutation.rs:28-30) by additions
-  const RFr bX = rx_mul(rx_unpack(q.rx_bg), ldr(&q.elements8[i]));  // beta g w^i [-1]
+  const RFr bX = rx_mul(rx_unpack(q.rx_bg[blk]), ldr(&q.elements[u]));  // beta s_m w_2n^u [-1]
   const RFr bX2 = rx_dbl(bX), bX4 = rx_dbl(bX2), bX8 = rx_dbl(bX4), bX16 = rx_dbl(bX8);
   const RFr bX7 = rx_sub(bX8, bX), bX13 = rx_add(rx_add(bX8, bX4), bX), bX17 = rx_add(bX16, bX);
   const RFr gm = rx_unpack(q.rx_gamma);  // [-1]
@@ -289,7 +291,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
     RFr num = t;
 #pragma unroll
     for (int l = 0; l < RxShape<FrCfg>::L; ++l) num.v[l] += perm.v[l];
-    stf(&q.out[i], rx_pack_canonical(rx_mul(num, rx_unpack(q.rx_vh[i & 7]))));
+    stf(&q.out[i], rx_pack_canonical(rx_mul(num, rx_unpack(q.rx_vh[2 * blk + (u & 1)]))));
   } else {
     stf(&q.out[i], rx_pack_canonical(rx_add(t, perm)));  // [1]
   }
@@ -298,9 +300,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 // out[i] = (out[i] + logic + fixed-base + variable-base terms) / v_h
 __global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t N = q.n8;
+  const uint64_t N = q.nq;
   if (i >= N) return;
-  const uint64_t nx = (i + 8) & (N - 1);
+  const uint64_t blk = i >> q.log_blk, u = i & ((1ull << q.log_blk) - 1);
+  const uint64_t nx = (blk << q.log_blk) + ((u + 2) & ((1ull << q.log_blk) - 1));
   // k_quotient left num at exponent +1 and the wire evaluations are at -1 (QuotientArgs):
   // back to the R domain for the packed arithmetic here
   auto ldw = [&](const Fr* p) { return fe_mul(ldf(p), q.rx_inv32); };
@@ -346,7 +349,22 @@ __global__ void __launch_bounds__(256) k_quotient_ext(QuotientArgs q) {
       t = fe_add(t, fe_mul(fe_mul(w, qv), q.var_sep));
     }
   }
-  stf(&q.out[i], fe_mul(t, q.vh_inv[i & 7]));
+  stf(&q.out[i], fe_mul(t, q.vh_inv[2 * blk + (u & 1)]));
+}
+
+// t from the three inverse block transforms (pk_coset3_combine, prover.hpp)
+__global__ void __launch_bounds__(256) k_coset3_combine(const Fr* __restrict__ in, uint64_t n2,
+                                                        Fr c1a, Fr c1b, Fr c1c, Fr c2a, Fr c2b,
+                                                        Fr c2c, Fr* __restrict__ out) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n2) return;
+  const RFr b0 = ldr(&in[k]), b1 = ldr(&in[n2 + k]), b2 = ldr(&in[2 * n2 + k]);  // R domain
+  stf(&out[k], rx_pack_canonical(rx_add(rx_add(b0, b1), b2)));
+  // constants in the R' domain: products land in the R domain
+  const RFr e1 = rx_add(rx_mul_add(b0, rx_unpack(c1a), b1, rx_unpack(c1b)), rx_mul(b2, rx_unpack(c1c)));
+  stf(&out[n2 + k], rx_pack_canonical(e1));
+  const RFr e2 = rx_add(rx_mul_add(b0, rx_unpack(c2a), b1, rx_unpack(c2b)), rx_mul(b2, rx_unpack(c2c)));
+  stf(&out[2 * n2 + k], rx_pack_canonical(e2));
 }
 
 // ------------------------------------------------------------ scaled table copy
@@ -566,8 +584,15 @@ int pk_scan(const Fr* in, Fr* out, uint64_t n, bool mul, bool suffix, bool exclu
   return PLK_OK;
 }
 
+int pk_coset3_combine(const Fr* in, uint64_t n2, const Fr* comb, Fr* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_coset3_combine, dim3(blocks_for(n2, 256)), dim3(256), 0, s, in, n2, comb[0],
+                     comb[1], comb[2], comb[3], comb[4], comb[5], out);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
 int pk_quotient(const QuotientArgs& q, hipStream_t s) {
-  const dim3 grid(blocks_for(q.n8, 256));
+  const dim3 grid(blocks_for(q.nq, 256));
   if (q.has_logic || q.has_fixed || q.has_var) {
     hipLaunchKernelGGL((k_quotient<false>), grid, dim3(256), 0, s, q);
     hipLaunchKernelGGL(k_quotient_ext, grid, dim3(256), 0, s, q);

@@ -99,8 +99,12 @@ static uint32_t choose_c(size_t n) {
 #define PLK_C_LARGE 16  // 17 (15 windows) measured slower end to end: its 2x buckets cost more in the sort and reduction kernels than the 6% fewer entries save
 #endif
   if (n >= (1u << 18)) return PLK_C_LARGE;
+// 2^14 .. 2^17 points: c = 15 (17 windows, top window 14 bits) against 13 (20 windows):
+// 2^16 bench 18.3 -> 19.4 M constraints/s (same box, two repetitions each,
+// tools/gpu_ab_c.sh); c = 16 is slower there (17.8 M: its 8x buckets against 20 % fewer
+// entries), and c = 14 leaves a 2-bit top window (a few huge buckets)
 #ifndef PLK_C_MID
-#define PLK_C_MID 13
+#define PLK_C_MID 15
 #endif
   if (n >= (1u << 14)) return PLK_C_MID;
   if (n >= (1u << 10)) return 10;
