@@ -482,7 +482,8 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
     s_ms, s_l, s_a, s_p = lanes[0].lane.msm_stats(reset=True)
     cbits = base.pp.last_msm_stats()[2]
     proofs = L if shard else L * world
-    transforms = "13 transforms (6 idft(n), 6 coset_dft(8n), 1 coset_idft(8n)) + 11 MSMs"
+    transforms = ("13 transforms (6 idft(n); 6 coset_dft and 1 coset_idft over the 6n quotient "
+                  "domain, each as 3 coset blocks of 2n) + 11 MSMs")
     result = {
         "metric": "PLONK prover constraints/sec (BLS12-381) at n=2^16 and 2^20, 1/2/4/8 GPUs",
         "value": n * steps * proofs / elapsed,
@@ -501,7 +502,8 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
             "workload": f"full Prover::create_proof at n=2^{k} (m = {base.gates} gates, 1 public "
                         f"input): synthesis + 5 rounds + 2 openings = {transforms} per proof "
                         "(the reference's 4 sigma dft(n) and L1's idft(n) + coset_dft(8n) are "
-                        "per-key constants here); host synthesis of the next proof overlaps "
+                        "per-key constants here; its 8n quotient coset is a 6n one here, same t "
+                        "and proof bytes, DESIGN §3); host synthesis of the next proof overlaps "
                         "the current GPU proof"
                         + (f"; {L} proofs in flight per GPU (plk_prover lanes sharing one key "
                            "and SRS)" if L > 1 else "")
@@ -528,12 +530,17 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
                             "durations overlap other lanes' kernels (not the kernel's own time)")
                if launches and acc_ms > 0 else None)
         traffic = load_pmc_traffic("k_accumulate")
+        traffic2 = load_pmc_traffic("k_accumulate", "hbm_bytes_per_launch_stream_corrected")
         result["roofline"] = {
             "bound": "hbm", "kernel": "k_accumulate", "achieved": solo["achieved_gbs"],
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": solo["achieved_gbs"] / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": ("profiles/pmc_traffic.json (rocprofv3 PMC pass of the default bench "
-                               "command, stored; raw TCC FETCH+WRITE, FETCH not doubled)")
+            "traffic": traffic, "traffic_fetch_doubled": traffic2,
+            "traffic_source": ("stored profile profiles/pmc_traffic.json (rocprofv3 --pmc "
+                               "FETCH_SIZE / WRITE_SIZE passes of the default bench command, "
+                               "per-launch average over the run); `traffic` = raw FETCH + WRITE, "
+                               "`traffic_fetch_doubled` applies the guide's gfx950 x2 for "
+                               "16-B/lane streams — this kernel's 96-B random gathers are an "
+                               "uncalibrated width, so the two bracket it")
             if traffic is not None else None,
             "algorithmic_bytes_per_launch": solo["algorithmic_bytes_per_launch"],
             "avg_launch_ms": solo["avg_launch_ms"], "launches": solo["launches"],
