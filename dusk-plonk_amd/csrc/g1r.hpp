@@ -185,6 +185,41 @@ __device__ __forceinline__ G1R g1r_lazy_finish(const G1R& p) {
   return r;
 }
 
+// ---- lazy full addition (both operands XYZZ), for the run-sum bucket reduction --------
+// add-2008-s with the normalisation deferred as in g1r_madd_lazy_sl. Operands: X in [0, 8p),
+// Y in [0, 4p), ZZ, ZZZ in [0, 2p), normalised limbs (g1r_lazy_finish outputs, g1r_infinity,
+// or results of this function); the result satisfies the same. Straight-line; the
+// exceptional cases (either operand at infinity, equal x) all give ZZ3 = ZZ1 ZZ2 P^2 = 0 and
+// are repaired after, by g1r_add_lazy.
+__device__ __forceinline__ G1R g1r_add_lazy_sl(const G1R& p, const G1R& q) {
+  const RFp U1 = rx_mul(p.X, q.ZZ);
+  const RFp U2 = rx_mul(q.X, p.ZZ);
+  const RFp S1 = rx_mul(p.Y, q.ZZZ);
+  const RFp S2 = rx_mul(q.Y, p.ZZZ);
+  const RFp P = rx_sub_u<FpCfg, 3>(U2, U1);  // (p, 5p)
+  const RFp R = rx_sub_u<FpCfg, 3>(S2, S1);  // (p, 5p)
+  const RFp PP = rx_sqr(P);
+  const RFp PPP = rx_mul(P, PP);
+  const RFp Q = rx_mul(U1, PP);
+  G1R r;
+  r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
+  r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), S1), PPP);
+  r.ZZ = rx_mul(rx_mul(p.ZZ, q.ZZ), PP);
+  r.ZZZ = rx_mul(rx_mul(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+__device__ __forceinline__ G1R g1r_add_lazy(const G1R& p, const G1R& q) {
+  const G1R r = g1r_add_lazy_sl(p, q);
+  if (rx_is_zero(r.ZZ)) {  // rare: an operand at infinity, or equal x (then X3 = R^2 + 6p)
+    if (g1r_is_inf(p)) return q;
+    if (g1r_is_inf(q)) return p;
+    if (rx_is_zero_u(r.X)) return g1r_dbl(g1r_lazy_finish(p));  // R == 0: p == q
+    return g1r_infinity();
+  }
+  return r;
+}
+
 // ---- packed memory <-> limbs (16-byte loads/stores of the 48-byte coordinates) -------
 __device__ __forceinline__ RFp ld_rfp(const uint32_t* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);

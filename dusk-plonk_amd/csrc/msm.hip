@@ -295,6 +295,235 @@ __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
         make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << kTaskShift));
 }
 
+// ---- wide bucket sets (B > kLdsBuckets, c >= 17): two-level radix sort ----------------
+// One LDS histogram cannot hold the buckets, and per-(workgroup, bucket) runs of ~1 entry
+// make a direct scatter write-amplified. Instead: (1) coarse bins of kFine consecutive
+// buckets — per-workgroup LDS histograms, a per-bin scan over the workgroups and a scatter
+// of (code, bucket) pairs into bin order (runs of ~100 entries per (workgroup, bin));
+// (2) one workgroup per bin counting-sorts its entries by bucket inside the bin's own
+// region (LDS counters, writes that stay in one L2), emitting the bucket offsets and the
+// per-bucket task counts on the way; (3) the task records, as k_make_tasks does.
+constexpr uint32_t kFineBits = 10;
+constexpr uint32_t kFine = 1u << kFineBits;  // buckets per coarse bin = threads of k_fine
+constexpr uint32_t kCoarseMax = 4096;        // coarse bins (B <= 2^22, c <= 23)
+constexpr uint32_t kRunBits = 4;             // bucket reduction: runs of 16 buckets per lane
+
+// Exclusive scan over the workgroup of K values per thread (wave shuffles, then the wave
+// totals through LDS); tot = the workgroup totals. sh: K * 32 words.
+template <int K>
+__device__ __forceinline__ void block_scan_excl(uint32_t (&v)[K], uint32_t (&tot)[K], uint32_t* sh) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t inc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) inc[k] = v[k];
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t t = __shfl_up(inc[k], o, 64);
+      if (lane >= o) inc[k] += t;
+    }
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) sh[k * 32 + wid] = inc[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    uint32_t base = 0, total = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+      const uint32_t s = sh[k * 32 + w];
+      base += w < wid ? s : 0u;
+      total += s;
+    }
+    v[k] = base + inc[k] - v[k];
+    tot[k] = total;
+  }
+  __syncthreads();
+}
+
+// Wide pass 1: per-workgroup histogram of the coarse bins (bucket >> kFineBits), written whole
+__global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg cfg, uint32_t NC,
+                                                        uint32_t* __restrict__ blockhist) {
+  __shared__ uint32_t hist[kCoarseMax];
+  const uint32_t slot = blockIdx.y;
+  uint32_t i0, i1;
+  slot_range(batch.len[slot], i0, i1);
+  const Fr* sc = batch.scalars[slot];
+  for (uint32_t b = threadIdx.x; b < NC; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    bool neg;
+    const Fr s = scalar_half(&sc[i], neg);
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) {
+      const int d = digit_at(s, w, cfg.c, carry);
+      if (d != 0) atomicAdd(&hist[((uint32_t)(d < 0 ? -d : d) - 1u) >> kFineBits], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* out = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * NC;
+  for (uint32_t b = threadIdx.x; b < NC; b += blockDim.x) out[b] = hist[b];
+}
+
+// Wide pass 2 (after k_block_scan over the bins): every workgroup scans the bin totals into
+// bin offsets (workgroup 0 also stores them), then each digit's (code, bucket) takes the next
+// slot of its bin in this workgroup's range.
+__global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCfg cfg, uint32_t NC,
+                                                           uint64_t n_srs,
+                                                           const uint32_t* __restrict__ ccounts,
+                                                           const uint32_t* __restrict__ blockhist,
+                                                           uint32_t* __restrict__ coarse_off,
+                                                           uint2* __restrict__ tmp, uint64_t tmp_stride) {
+  __shared__ uint32_t hist[kCoarseMax];
+  __shared__ uint32_t sh[32];
+  const uint32_t slot = blockIdx.y, tid = threadIdx.x;
+  const uint32_t* cc = ccounts + (size_t)slot * NC;
+  const uint32_t* bh = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * NC;
+  uint32_t* co = coarse_off + (size_t)slot * (NC + 1);
+  uint32_t loc[4], v[1], tot[1];
+  v[0] = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint32_t b = 4 * tid + q;
+    loc[q] = b < NC ? cc[b] : 0u;
+    v[0] += loc[q];
+  }
+  block_scan_excl<1>(v, tot, sh);
+  uint32_t run = v[0];
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint32_t b = 4 * tid + q;
+    if (b < NC) {
+      if (blockIdx.x == 0) co[b] = run;
+      hist[b] = run + bh[b];
+    }
+    run += loc[q];
+  }
+  if (blockIdx.x == 0 && tid == 0) co[NC] = tot[0];
+  __syncthreads();
+  uint32_t i0, i1;
+  slot_range(batch.len[slot], i0, i1);
+  const Fr* sc = batch.scalars[slot];
+  uint2* out = tmp + (size_t)slot * tmp_stride;
+  for (uint32_t i = i0 + tid; i < i1; i += blockDim.x) {
+    bool neg;
+    const Fr s = scalar_half(&sc[i], neg);
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) {
+      const int d = digit_at(s, w, cfg.c, carry);
+      if (d != 0) {
+        const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
+        const uint32_t pos = atomicAdd(&hist[b >> kFineBits], 1u);
+        out[pos] = make_uint2((uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u), b);
+      }
+    }
+  }
+}
+
+// Wide pass 3: one workgroup per (bin, slot), one thread per bucket of the bin. Counting sort
+// of the bin's entries by bucket into its own region of `sorted`; bucket offsets (global),
+// per-bucket task and full-task offsets relative to the bin, the bin's totals and the
+// global histogram of tail lengths (for the execution order of the tasks).
+__global__ void __launch_bounds__(kFine) k_fine(uint32_t B, uint32_t NC, uint32_t chunk,
+                                                const uint32_t* __restrict__ coarse_off,
+                                                const uint2* __restrict__ tmp, uint64_t tmp_stride,
+                                                uint32_t* __restrict__ sorted, uint64_t sorted_stride,
+                                                uint32_t* __restrict__ offsets,
+                                                uint32_t* __restrict__ task_rel,
+                                                uint32_t* __restrict__ full_rel,
+                                                uint32_t* __restrict__ bin_tot,
+                                                uint32_t* __restrict__ len_count) {
+  __shared__ uint32_t cnt[kFine];
+  __shared__ uint32_t s_len[kChunkMax];
+  __shared__ uint32_t sh[3 * 32];
+  const uint32_t slot = blockIdx.y, bin = blockIdx.x, tid = threadIdx.x;
+  const uint32_t lo = coarse_off[(size_t)slot * (NC + 1) + bin];
+  const uint32_t hi = coarse_off[(size_t)slot * (NC + 1) + bin + 1];
+  const uint2* in = tmp + (size_t)slot * tmp_stride;
+  cnt[tid] = 0;
+  if (tid < kChunkMax) s_len[tid] = 0;
+  __syncthreads();
+  for (uint32_t e = lo + tid; e < hi; e += kFine) atomicAdd(&cnt[in[e].y & (kFine - 1)], 1u);
+  __syncthreads();
+  const uint32_t c = cnt[tid];
+  if (c % chunk) atomicAdd(&s_len[c % chunk], 1u);
+  uint32_t v[3] = {c, (c + chunk - 1) / chunk, c / chunk}, tot[3];
+  block_scan_excl<3>(v, tot, sh);  // its barriers also order the s_len atomics and cnt reads
+  const uint32_t b = bin * kFine + tid;  // B = NC * kFine
+  offsets[(size_t)slot * (B + 1) + b] = lo + v[0];
+  task_rel[(size_t)slot * B + b] = v[1];
+  full_rel[(size_t)slot * B + b] = v[2];
+  if (tid == 0) {
+    bin_tot[(size_t)slot * 2 * NC + bin] = tot[1];
+    bin_tot[(size_t)slot * 2 * NC + NC + bin] = tot[2];
+    if (bin == NC - 1) offsets[(size_t)slot * (B + 1) + B] = hi;
+  }
+  if (tid < kChunkMax && s_len[tid]) atomicAdd(&len_count[(size_t)slot * kChunkMax + tid], s_len[tid]);
+  cnt[tid] = v[0];  // cursor of bucket tid, relative to lo
+  __syncthreads();
+  uint32_t* out = sorted + (size_t)slot * sorted_stride + lo;
+  for (uint32_t e = lo + tid; e < hi; e += kFine) {
+    const uint2 x = in[e];
+    out[atomicAdd(&cnt[x.y & (kFine - 1)], 1u)] = x.x;
+  }
+}
+
+// Wide pass 4: task records in the layout of k_make_tasks (full tasks first, bucket order;
+// tails grouped by length, longest first). Bin bases are sums of the bin totals below.
+__global__ void __launch_bounds__(kFine) k_make_tasks_wide(uint32_t B, uint32_t NC, uint32_t chunk,
+                                                           const uint32_t* __restrict__ offsets,
+                                                           const uint32_t* __restrict__ task_rel,
+                                                           const uint32_t* __restrict__ full_rel,
+                                                           const uint32_t* __restrict__ bin_tot,
+                                                           const uint32_t* __restrict__ len_count,
+                                                           uint32_t* __restrict__ len_fill,
+                                                           uint32_t* __restrict__ task_off,
+                                                           uint2* __restrict__ tasks,
+                                                           uint64_t task_stride) {
+  __shared__ uint32_t s_cnt[kChunkMax], s_base[kChunkMax], s_lc[kChunkMax], sh[4 * 32];
+  const uint32_t slot = blockIdx.y, bin = blockIdx.x, tid = threadIdx.x;
+  const uint32_t* bt = bin_tot + (size_t)slot * 2 * NC;
+  uint32_t v[4] = {0, 0, 0, 0}, tot[4];
+  for (uint32_t q = tid; q < NC; q += blockDim.x) {
+    const uint32_t a = bt[q], f = bt[NC + q];
+    v[0] += q < bin ? a : 0u;
+    v[1] += q < bin ? f : 0u;
+    v[2] += a;
+    v[3] += f;
+  }
+  if (tid < kChunkMax) {
+    s_cnt[tid] = 0;
+    s_lc[tid] = len_count[(size_t)slot * kChunkMax + tid];
+  }
+  block_scan_excl<4>(v, tot, sh);
+  const uint32_t task_base = tot[0], full_base = tot[1], task_total = tot[2], full_total = tot[3];
+  const uint32_t b = bin * kFine + tid;
+  const uint32_t* off = offsets + (size_t)slot * (B + 1);
+  const uint32_t start = off[b], cnt = off[b + 1] - start;
+  const uint32_t t0 = task_base + task_rel[(size_t)slot * B + b];
+  const uint32_t f0 = full_base + full_rel[(size_t)slot * B + b];
+  task_off[(size_t)slot * (B + 1) + b] = t0;
+  if (b == B - 1) task_off[(size_t)slot * (B + 1) + B] = task_total;
+  const uint32_t nfull = cnt / chunk, tail = cnt - nfull * chunk;
+  uint32_t rank = 0;
+  if (tail) rank = atomicAdd(&s_cnt[tail], 1u);
+  __syncthreads();
+  if (tid < kChunkMax && s_cnt[tid]) {
+    uint32_t base = full_total;  // tails of length l start after all longer tails
+    for (uint32_t l = tid + 1; l < kChunkMax; ++l) base += s_lc[l];
+    s_base[tid] = base + atomicAdd(&len_fill[(size_t)slot * kChunkMax + tid], s_cnt[tid]);
+  }
+  __syncthreads();
+  tasks += (size_t)slot * task_stride;
+  for (uint32_t t = 0; t < nfull; ++t)
+    tasks[f0 + t] = make_uint2(start + t * chunk, (t0 + t) | ((chunk - 1) << kTaskShift));
+  if (tail)
+    tasks[s_base[tail] + rank] =
+        make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << kTaskShift));
+}
+
 #ifndef PLK_ACC_WAVES
 #define PLK_ACC_WAVES 1  // min waves per SIMD requested from the register allocator
 #endif
@@ -386,6 +615,63 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
   }
 }
 
+// Wide bucket sets, reduction step 1: lane r owns the run of K = 2^kRunBits buckets
+// b = rK + t. It forms each bucket sum S_b from the bucket's accumulation partials and keeps
+// running sums from the top of the run, R = sum_t S_(rK+t) and T = sum_t (t + 1) S_(rK+t),
+// then emits Y_r = R and Z_r = T - K R:
+//   sum_b (b + 1) S_b = sum_r (T_r + rK R_r) = K sum_r (r + 1) Y_r + sum_r Z_r,
+// 2 additions per bucket with every lane busy (the bit-sum trees over 2^19 buckets left most
+// lanes idle); the first sum is the bit-sum reduction over the runs, the second a plain sum.
+// The run's tail outside the hot loop (not inlined: one call per 16 buckets): Z = T - K R
+__device__ __noinline__ void runsum_tail(G1R R, G1R T, G1xyzz* __restrict__ z) {
+  for (uint32_t i = 0; i < kRunBits; ++i) R = g1r_dbl(R);
+  st_g1r(z, g1r_lazy_finish(g1r_add_lazy(T, g1r_neg(R))));
+}
+
+__global__ void __launch_bounds__(256) k_runsum(const uint32_t* __restrict__ task_off, uint32_t B,
+                                                uint64_t task_stride,
+                                                const G1xyzz* __restrict__ partials,
+                                                G1xyzz* __restrict__ ys, G1xyzz* __restrict__ zs) {
+  constexpr uint32_t K = 1u << kRunBits;
+  const uint32_t slot = blockIdx.y, NR = B >> kRunBits;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= NR) return;
+  task_off += (size_t)slot * (B + 1);
+  partials += (size_t)slot * task_stride;
+  // One addition per step, operands selected per lane — R += (next partial of the bucket),
+  // or at the bucket's end T += R — so the wave runs ONE inlined addition in lock step
+  // whatever the partial counts of its lanes' buckets (S_b never formed: R += S_b is the
+  // same sum taken partial by partial).
+  G1R R = g1r_infinity(), T = g1r_infinity();
+  uint32_t t = K - 1;
+  uint32_t p = task_off[r * K + t], pe = task_off[r * K + t + 1];  // bucket t's partials
+  for (;;) {
+    const bool part = p < pe;
+    G1R a, b;
+    if (part) {
+      a = R;
+      b = ld_g1r(&partials[p]);
+    } else {
+      a = T;
+      b = R;
+    }
+    const G1R c = g1r_add_lazy(a, b);
+    if (part) {
+      R = c;
+      ++p;
+    } else {
+      T = c;
+      if (t == 0) break;
+      --t;
+      pe = task_off[r * K + t + 1];
+      p = task_off[r * K + t];
+    }
+  }
+  R = g1r_lazy_finish(R);
+  st_g1r(&ys[(size_t)slot * NR + r], R);
+  runsum_tail(R, T, &zs[(size_t)slot * NR + r]);
+}
+
 // Bucket reduction sum_b (b+1) S_b, split per workgroup g of 256 buckets b = 256g + u,
 // u = 16a + c (a, c < 16):
 //   sum_u (256g + u + 1) S_(g,u) = sum_(j<8) 2^j T_j(g) + (256g + 1) A_g,
@@ -396,8 +682,9 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
 // the 1 144 of bit sums taken over the buckets themselves.
 // k_bitsum1 (one workgroup of 256 lanes per g): the bucket sums S (k_bucket_sum), the 32
 // row / column sums (8 lanes each: one addition, then a 3-level LDS tree),
-// then the 9 outputs from them (wave 0). out[slot][g][0..7] = T_j(g), [8] = A_g.
-constexpr uint32_t kBitsumOut = 9;
+// then the 9 outputs from them (wave 0). out[slot][g][0..7] = T_j(g), [8] = A_g; with `zin`
+// (wide bucket sets) also [9] = the plain sum of the group's 256 Z values (k_runsum).
+constexpr uint32_t kBitsumOut = 10;
 
 // k-th of the 8 indices in [0, 16) with bit j set
 __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
@@ -405,6 +692,7 @@ __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
 }
 
 __global__ void __launch_bounds__(256) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
+                                                 const G1xyzz* __restrict__ zin,
                                                  G1xyzz* __restrict__ out) {
   __shared__ G1xyzz sh[256 + 32];  // [0, 256): buckets, then tree partials; [256, 288): rows, columns
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
@@ -458,19 +746,34 @@ __global__ void __launch_bounds__(256) k_bitsum1(uint32_t B, const G1xyzz* __res
     }
     if (e == 0) out[s] = sh[tid];
   }
+  if (zin) {  // plain tree sum of the group's Z values
+    __syncthreads();
+    const uint32_t b = g * 256 + tid;
+    if (b < B) sh[tid] = zin[(size_t)slot * B + b];
+    else st_g1r(&sh[tid], g1r_infinity());
+    __syncthreads();
+    for (uint32_t h = 128; h >= 1; h >>= 1) {
+      if (tid < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
+      __syncthreads();
+    }
+    if (tid == 0) out[9] = sh[0];
+  }
 }
 
 // Workgroup j of slot: T_j = sum_g T_j(g) for 0 < j < 8; T_0 = sum_g (T_0(g) + A_g);
-// T_(8+i) = sum_(g: bit i of g) A_g.
+// T_(8+i) = sum_(g: bit i of g) A_g; j = nbits (wide bucket sets): sum_g Z_g.
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
-                                                 uint32_t nbits, G1xyzz* __restrict__ out) {
+                                                 uint32_t nbits, uint32_t nout,
+                                                 G1xyzz* __restrict__ out) {
   __shared__ G1xyzz sh[256];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
   in += (size_t)slot * G * kBitsumOut;
   G1R acc = g1r_infinity();
   for (uint32_t g = tid; g < G; g += 256) {
     const G1xyzz* e = &in[(size_t)g * kBitsumOut];
-    if (j < 8) {
+    if (j == nbits) {
+      acc = g1r_add(acc, ld_g1r(&e[9]));
+    } else if (j < 8) {
       acc = g1r_add(acc, ld_g1r(&e[j]));
       if (j == 0) acc = g1r_add(acc, ld_g1r(&e[8]));
     } else if ((g >> (j - 8)) & 1u) {
@@ -483,7 +786,7 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
     if (tid < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
     __syncthreads();
   }
-  if (tid == 0) out[(size_t)slot * nbits + j] = sh[0];
+  if (tid == 0) out[(size_t)slot * nout + j] = sh[0];
 }
 
 // flag[slot] |= any nonzero scalar in [len, check_len)  (commit degree check)
@@ -518,21 +821,35 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
   len = std::max(len, w.cap_len);
   slots = std::max(slots, w.cap_slots);
   const size_t B = (size_t)1 << (s->c - 1);
+  const bool wide = B > kLdsBuckets;
+  const size_t NC = B >> kFineBits, NR = B >> kRunBits;
+  if (wide && NC > kCoarseMax) return PLK_E_ARG;
   const size_t entries = (size_t)s->windows * len;
   const size_t max_tasks = entries / kChunkMin + B + 1;
-  const size_t G = (B + 255) / 256;
+  const size_t G = ((wide ? NR : B) + 255) / 256;
   if (max_tasks >= ((size_t)1 << kTaskShift)) return PLK_E_ARG;  // task records: partial index bits
   int st;
-  if ((st = w.counts.alloc(slots * B * 4))) return st;
+  const size_t hb = wide ? NC : B;  // histogram bins: coarse bins or buckets
+  if ((st = w.counts.alloc(slots * hb * 4))) return st;
   if ((st = w.offsets.alloc(slots * (B + 1) * 4))) return st;
   if ((st = w.task_off.alloc(slots * (B + 1) * 4))) return st;
-  if ((st = w.blockhist.alloc(slots * kHistBlocksMax * B * 4))) return st;
+  if ((st = w.blockhist.alloc(slots * kHistBlocksMax * hb * 4))) return st;
   if ((st = w.full_off.alloc(slots * B * 4))) return st;
   if ((st = w.len_cur.alloc(slots * kChunkMax * 4))) return st;
   if ((st = w.sorted.alloc(slots * (entries + 1) * 4))) return st;
   if ((st = w.tasks.alloc(slots * max_tasks * sizeof(uint2)))) return st;
   if ((st = w.partials.alloc(slots * max_tasks * sizeof(G1xyzz)))) return st;
-  if ((st = w.bsum.alloc(slots * B * sizeof(G1xyzz)))) return st;
+  if (wide) {
+    if ((st = w.tmp.alloc(slots * entries * sizeof(uint2)))) return st;
+    if ((st = w.task_rel.alloc(slots * B * 4))) return st;
+    if ((st = w.bin_tot.alloc(slots * 2 * NC * 4))) return st;
+    if ((st = w.len_fill.alloc(slots * kChunkMax * 4))) return st;
+    if ((st = w.coarse_off.alloc(slots * (NC + 1) * 4))) return st;
+    if ((st = w.ys.alloc(slots * NR * sizeof(G1xyzz)))) return st;
+    if ((st = w.zs.alloc(slots * NR * sizeof(G1xyzz)))) return st;
+  } else {
+    if ((st = w.bsum.alloc(slots * B * sizeof(G1xyzz)))) return st;
+  }
   if ((st = w.bits1.alloc(slots * G * kBitsumOut * sizeof(G1xyzz)))) return st;
   if ((st = w.bits2.alloc(slots * 32 * sizeof(G1xyzz)))) return st;  // nbits <= 32
   if ((st = w.flag.alloc(slots * 4 + 16))) return st;
@@ -575,12 +892,20 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   if ((st = ws_reserve(s, w, max_len ? max_len : 1, (uint32_t)count))) return st;
   const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1)};
   const uint32_t B = cfg.B;
-  const uint32_t G = cdiv(B, 256);  // a power of two
+  // wide bucket sets: two-level sort and run-sum reduction; the bit sums then run over the
+  // NR = B / 2^kRunBits runs instead of the buckets
+  const bool wide = B > kLdsBuckets;
+  const uint32_t NC = B >> kFineBits, NR = B >> kRunBits;
+  const uint32_t G = cdiv(wide ? NR : B, 256);  // a power of two
   const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
+  const uint32_t nout = nbits + (wide ? 1u : 0u);         // + the plain sum of the Z values
   const uint32_t slots = (uint32_t)count;
-  // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads
-  const uint32_t chunk = (uint32_t)std::min<size_t>(
-      kChunkMax, std::max<size_t>(kChunkMin, total_entries / PLK_CHUNK_TARGET));
+  // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads; wide
+  // sets have few entries per bucket and enough tasks anyway: one task per bucket
+  const uint32_t chunk =
+      wide ? kChunkMax
+           : (uint32_t)std::min<size_t>(kChunkMax,
+                                        std::max<size_t>(kChunkMin, total_entries / PLK_CHUNK_TARGET));
   const size_t max_tasks_used = (size_t)s->windows * max_len / chunk + B;
   // 256 workgroups per slot: fewer give longer per-bucket write runs in k_scatter but lose
   // more parallelism than they gain (measured 2.77 / 2.79 / 3.02 / 4.52 ms per proof at
@@ -593,29 +918,59 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
                        batch, w.flag.as<uint32_t>());
   }
-  const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
-  if (max_len) {
-    hipLaunchKernelGGL(k_hist, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream, batch,
-                       cfg, w.blockhist.as<uint32_t>());
+  if (wide) {
+    PLK_HIP_TRY(hipMemsetAsync(w.len_cur.ptr, 0, (size_t)slots * kChunkMax * 4, stream));
+    PLK_HIP_TRY(hipMemsetAsync(w.len_fill.ptr, 0, (size_t)slots * kChunkMax * 4, stream));
+    if (max_len) {
+      hipLaunchKernelGGL(k_chist, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
+                         cfg, NC, w.blockhist.as<uint32_t>());
+    } else {
+      PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * NC * 4, stream));
+    }
+    hipLaunchKernelGGL(k_block_scan, dim3(cdiv(NC, 256), slots), dim3(256), 0, stream,
+                       w.blockhist.as<uint32_t>(), hist_blocks, NC, w.counts.as<uint32_t>());
+    hipLaunchKernelGGL(k_cscatter, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
+                       cfg, NC, (uint64_t)s->n, (const uint32_t*)w.counts.as<uint32_t>(),
+                       (const uint32_t*)w.blockhist.as<uint32_t>(), w.coarse_off.as<uint32_t>(),
+                       w.tmp.as<uint2>(), (uint64_t)(w.sorted_stride - 1));
+    hipLaunchKernelGGL(k_fine, dim3(NC, slots), dim3(kFine), 0, stream, B, NC, chunk,
+                       (const uint32_t*)w.coarse_off.as<uint32_t>(), (const uint2*)w.tmp.as<uint2>(),
+                       (uint64_t)(w.sorted_stride - 1), w.sorted.as<uint32_t>(),
+                       (uint64_t)w.sorted_stride, w.offsets.as<uint32_t>(),
+                       w.task_rel.as<uint32_t>(), w.full_off.as<uint32_t>(),
+                       w.bin_tot.as<uint32_t>(), w.len_cur.as<uint32_t>());
+    hipLaunchKernelGGL(k_make_tasks_wide, dim3(NC, slots), dim3(kFine), 0, stream, B, NC, chunk,
+                       (const uint32_t*)w.offsets.as<uint32_t>(),
+                       (const uint32_t*)w.task_rel.as<uint32_t>(),
+                       (const uint32_t*)w.full_off.as<uint32_t>(),
+                       (const uint32_t*)w.bin_tot.as<uint32_t>(),
+                       (const uint32_t*)w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>(),
+                       w.task_off.as<uint32_t>(), w.tasks.as<uint2>(), (uint64_t)w.task_stride);
   } else {
-    PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * B * 4, stream));
+    const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
+    if (max_len) {
+      hipLaunchKernelGGL(k_hist, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream, batch,
+                         cfg, w.blockhist.as<uint32_t>());
+    } else {
+      PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * B * 4, stream));
+    }
+    hipLaunchKernelGGL(k_block_scan, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
+                       w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>());
+    hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
+                       w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
+                       w.task_off.as<uint32_t>(), w.full_off.as<uint32_t>(),
+                       w.len_cur.as<uint32_t>());
+    if (max_len) {
+      hipLaunchKernelGGL(k_scatter, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream,
+                         batch, cfg, (uint64_t)s->n, w.offsets.as<uint32_t>(),
+                         w.blockhist.as<uint32_t>(), w.sorted.as<uint32_t>(),
+                         (uint64_t)w.sorted_stride);
+    }
+    hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
+                       w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),
+                       w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>(), B, chunk,
+                       w.tasks.as<uint2>(), (uint64_t)w.task_stride);
   }
-  hipLaunchKernelGGL(k_block_scan, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
-                     w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>());
-  hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
-                     w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
-                     w.task_off.as<uint32_t>(), w.full_off.as<uint32_t>(),
-                     w.len_cur.as<uint32_t>());
-  if (max_len) {
-    hipLaunchKernelGGL(k_scatter, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream,
-                       batch, cfg, (uint64_t)s->n, w.offsets.as<uint32_t>(),
-                       w.blockhist.as<uint32_t>(), w.sorted.as<uint32_t>(),
-                       (uint64_t)w.sorted_stride);
-  }
-  hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
-                     w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),
-                     w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>(), B, chunk,
-                     w.tasks.as<uint2>(), (uint64_t)w.task_stride);
   // start / stop events stamped by the dispatch itself (its execution, as rocprofv3 times
   // it), not by the stream: with several lanes on the GPU a stream event would also count
   // the time the kernel waits behind other lanes' kernels
@@ -635,7 +990,11 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                             (const uint8_t*)s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
     }
   }
-  {
+  if (wide) {
+    hipLaunchKernelGGL(k_runsum, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream,
+                       (const uint32_t*)w.task_off.as<uint32_t>(), B, (uint64_t)w.task_stride,
+                       (const G1xyzz*)w.partials.as<G1xyzz>(), w.ys.as<G1xyzz>(), w.zs.as<G1xyzz>());
+  } else {
     // lanes per bucket: until each lane adds ~PLK_LANE_PARTIALS partials (partials per bucket = entries /
     // chunk + 1 tail) or the grid holds 2^17 lanes (the tree levels cost a full addition
     // per lane, so an already full chip gains nothing from more lanes per bucket)
@@ -646,13 +1005,14 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
                        w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
   }
-  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, B, w.bsum.as<G1xyzz>(),
-                     w.bits1.as<G1xyzz>());
-  hipLaunchKernelGGL(k_bitsum2, dim3(nbits, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
-                     G, nbits, w.bits2.as<G1xyzz>());
+  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, wide ? NR : B,
+                     (const G1xyzz*)(wide ? w.ys.as<G1xyzz>() : w.bsum.as<G1xyzz>()),
+                     (const G1xyzz*)(wide ? w.zs.as<G1xyzz>() : nullptr), w.bits1.as<G1xyzz>());
+  hipLaunchKernelGGL(k_bitsum2, dim3(nout, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
+                     G, nbits, nout, w.bits2.as<G1xyzz>());
   PLK_HIP_TRY(hipGetLastError());
 
-  const size_t t_count = (size_t)slots * nbits;
+  const size_t t_count = (size_t)slots * nout;
   if ((st = w.host_out.alloc(t_count * sizeof(G1xyzz) + 2 * slots * sizeof(uint32_t)))) return st;
   G1xyzz* T = w.host_out.as<G1xyzz>();
   uint32_t* flag = reinterpret_cast<uint32_t*>(T + t_count);
@@ -688,7 +1048,11 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     G1xyzz acc = xyzz_infinity();
     for (int j = (int)nbits - 1; j >= 0; --j) {
       acc = xyzz_dbl(acc);
-      acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nbits + j]));
+      acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + j]));
+    }
+    if (wide) {  // sum over the runs: K * sum_r (r + 1) Y_r + sum_r Z_r (k_runsum)
+      for (uint32_t i = 0; i < kRunBits; ++i) acc = xyzz_dbl(acc);
+      acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + nbits]));
     }
     Fp x, y;
     const bool fin = xyzz_to_affine(acc, x, y);

@@ -94,6 +94,19 @@ __global__ void __launch_bounds__(256) k_table_to_rx(G1Affine* __restrict__ tab,
 
 // Window size for an SRS of n points (bucket count 2^(c-1); table W*n, W = ceil(255/c)).
 static uint32_t choose_c(size_t n) {
+  // PLK_MSM_C (tests, experiments): a fixed window size for every SRS prepared afterwards
+  if (const char* e = getenv("PLK_MSM_C")) {
+    const int c = atoi(e);
+    if (c >= 8 && c <= 23) return (uint32_t)c;
+  }
+  // 2^20 points and up: c = 20, 13 windows (16 at c = 16). Entries N * W fall 19 %; the
+  // 2^19 buckets (~26 entries each) go through the wide-set sort and the run-sum
+  // reduction (msm.hip), ~2.2 additions per bucket. Per MSM: N * ceil(255 / c) mixed
+  // additions + ~2.2 * 2^(c-1) full ones is smallest at c = 20 for N = 2^20.
+#ifndef PLK_C_HUGE
+#define PLK_C_HUGE 20
+#endif
+  if (n >= (1u << 20)) return PLK_C_HUGE;
   // c = 17: 15 windows of the half-range scalars (msm.hip scalar_half) against 16 at c = 16
 #ifndef PLK_C_LARGE
 #define PLK_C_LARGE 16  // 17 (15 windows) measured slower end to end: its 2x buckets cost more in the sort and reduction kernels than the 6% fewer entries save

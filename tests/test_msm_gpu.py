@@ -123,9 +123,9 @@ def test_commit_dev_and_stats(plk, gpu_ctx, oracle):
 
 @pytest.mark.slow
 def test_msm_2_20_vs_oracle(plk, gpu_ctx, oracle):
-    """BASELINE configs[2] at its full size: a 2^20-point MSM over the bench SRS (c = 16, 16
-    windows of the window table) bit-exact against the C oracle's Pippenger, random and
-    sparse scalars."""
+    """BASELINE configs[2] at its full size: a 2^20-point MSM over the bench SRS (c = 20: 13
+    windows of the window table, the wide-bucket sort and run-sum reduction) bit-exact
+    against the C oracle's Pippenger, random and sparse scalars."""
     import os
     n = 1 << 20
     pp = plk.PlonkParams.setup(20, random_fr(1, seed=20)[0], gpu_ctx)
@@ -195,3 +195,54 @@ def test_commit_batch_dev(plk, gpu_ctx, oracle):
                               torch.cuda.current_stream().cuda_stream)
     for i, p in enumerate(many):
         assert np.array_equal(out[i].words, oracle.msm(pts[:64], p)), i
+
+
+@pytest.mark.parametrize("c,logn", [(17, 10), (20, 12), (18, 14), (20, 16)])
+def test_msm_wide_buckets_vs_oracle(plk, gpu_ctx, oracle, monkeypatch, c, logn):
+    """Wide bucket sets (2^(c-1) > 32 K buckets: the two-level radix sort, the per-bin
+    counting sort and the run-sum bucket reduction of msm.hip) at small sizes, forced with
+    PLK_MSM_C: most buckets empty or single, skewed and adversarial scalar sets, batches."""
+    import torch
+    monkeypatch.setenv("PLK_MSM_C", str(c))
+    n = 1 << logn
+    tau = random_fr(1, seed=300 + logn)[0]
+    pp = plk.PlonkParams.setup(logn, tau, gpu_ctx, n_points=n + 8)
+    pts = pp.points()
+    sc = random_fr(n, seed=400 + logn)
+    cases = {
+        "random": sc,
+        "all_one": np.tile(fr_int(1), (n, 1)),
+        "all_same": np.tile(sc[:1], (n, 1)),
+        "tiny": P.fr_vec_to_np([i % 5 for i in range(n)]),
+        "sparse": np.where((np.arange(n) % 17 == 0)[:, None], sc, 0).astype(np.uint64),
+        "minus_one": np.tile(fr_int(P.R_MOD - 1), (n, 1)),
+        "high_bits": P.fr_vec_to_np([(1 << 253) + 7 * i for i in range(n)]),
+    }
+    for name, s in cases.items():
+        assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), name
+    # a batch of independent commits (slots) with different lengths and a degree error
+    lens = [n, n + 3, 17, n // 2, 1]
+    polys = [random_fr(m, seed=500 + i) for i, m in enumerate(lens)]
+    polys[4][:] = 0
+    bad = random_fr(n + 20, seed=599)
+    devs = [torch.from_numpy(p.view(np.int64)).cuda() for p in polys + [bad]]
+    torch.cuda.synchronize()
+    res = pp.commit_batch_dev([(d.data_ptr(), d.shape[0]) for d in devs],
+                              torch.cuda.current_stream().cuda_stream, raise_on_error=False)
+    for i, p in enumerate(polys):
+        assert np.array_equal(res[i].words, oracle.msm(pts[: p.shape[0]], p)), i
+    assert isinstance(res[-1], plk.PlonkError) and res[-1].status == plk.PLK_E_DEGREE
+
+
+@pytest.mark.parametrize("tau", [1, P.R_MOD - 1])
+def test_msm_wide_buckets_repeated_points(plk, gpu_ctx, oracle, monkeypatch, tau):
+    """Wide bucket sets with tau = +-1 (every SRS point G or -G): equal and opposite points
+    meet in the accumulation and the run sums (doubling / infinity branches)."""
+    monkeypatch.setenv("PLK_MSM_C", "20")
+    n = 1 << 10
+    pp = plk.PlonkParams.setup(10, fr_int(tau)[0], gpu_ctx, n_points=n)
+    pts = pp.points()
+    sc = random_fr(n, seed=79)
+    few = np.tile(random_fr(3, seed=80), (n // 3 + 1, 1))[:n].copy()
+    for name, s in {"random": sc, "three_values": few, "all_one": np.tile(fr_int(1), (n, 1))}.items():
+        assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), name
