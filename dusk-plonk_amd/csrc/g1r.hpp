@@ -192,32 +192,70 @@ __device__ __forceinline__ G1R g1r_lazy_finish(const G1R& p) {
 // exceptional cases (either operand at infinity, equal x) all give ZZ3 = ZZ1 ZZ2 P^2 = 0 and
 // are repaired after, by g1r_add_lazy.
 __device__ __forceinline__ G1R g1r_add_lazy_sl(const G1R& p, const G1R& q) {
+  // ordered so that the operands die early: X1, X2 after P, Y1, Y2 after R, the Z's after
+  // their products
   const RFp U1 = rx_mul(p.X, q.ZZ);
-  const RFp U2 = rx_mul(q.X, p.ZZ);
+  const RFp P = rx_sub_u<FpCfg, 3>(rx_mul(q.X, p.ZZ), U1);  // U2 - U1 + 3p in (p, 5p)
   const RFp S1 = rx_mul(p.Y, q.ZZZ);
-  const RFp S2 = rx_mul(q.Y, p.ZZZ);
-  const RFp P = rx_sub_u<FpCfg, 3>(U2, U1);  // (p, 5p)
-  const RFp R = rx_sub_u<FpCfg, 3>(S2, S1);  // (p, 5p)
+  const RFp R = rx_sub_u<FpCfg, 3>(rx_mul(q.Y, p.ZZZ), S1);  // S2 - S1 + 3p in (p, 5p)
+  const RFp ZZ12 = rx_mul(p.ZZ, q.ZZ);
+  const RFp ZZZ12 = rx_mul(p.ZZZ, q.ZZZ);
   const RFp PP = rx_sqr(P);
   const RFp PPP = rx_mul(P, PP);
   const RFp Q = rx_mul(U1, PP);
   G1R r;
+  r.ZZ = rx_mul(ZZ12, PP);
+  r.ZZZ = rx_mul(ZZZ12, PPP);
   r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
   r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), S1), PPP);
-  r.ZZ = rx_mul(rx_mul(p.ZZ, q.ZZ), PP);
-  r.ZZZ = rx_mul(rx_mul(p.ZZZ, q.ZZZ), PPP);
   return r;
+}
+
+// dbl-2008-s-1 on a lazy operand (X < 8p, Y < 4p, ZZ, ZZZ < 2p; normalised limbs) with the
+// lazy normalisation of g1r_madd_lazy_sl: result X3 in (2p, 8p), Y3 < 2p. Infinity (ZZ = 0)
+// stays infinity (ZZ3 = V ZZ); G1 has no 2-torsion, so Y != 0 otherwise.
+__device__ __forceinline__ G1R g1r_dbl_lazy(const G1R& p) {
+  RFp U, M;
+#pragma unroll
+  for (int i = 0; i < RxShape<FpCfg>::L; ++i) U.v[i] = p.Y.v[i] << 1;  // 2Y < 8p, limbs < 2^29
+  const RFp V = rx_sqr(U);
+  const RFp W = rx_mul(U, V);
+  const RFp S = rx_mul(p.X, V);
+  const RFp X2 = rx_sqr(p.X);
+#pragma unroll
+  for (int i = 0; i < RxShape<FpCfg>::L; ++i) M.v[i] = X2.v[i] * 3u;  // 3X^2 < 6p, limbs < 2^30
+  G1R r;
+  r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(M), rx_zero<FpCfg>(), S);  // M^2 + 6p - 2S in (2p, 8p)
+  // Y3 = M (S - X3) - W Y = M (S - X3 + 10p) + (5p - Y) W, one reduction (bounds as in
+  // g1r_madd_lazy_sl: M limbs < 3 * 2^28, value < 6p)
+  r.Y = rx_mul_add(M, rx_sub_u<FpCfg, 10>(S, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), W);
+  r.ZZ = rx_mul(V, p.ZZ);
+  r.ZZZ = rx_mul(W, p.ZZZ);
+  return r;
+}
+
+// The rare path's arithmetic is made to depend on an opaque zero defined here: without it
+// LLVM speculates the doubling (~3 300 mads) above the branch and selects its result,
+// paying it on every addition.
+__device__ __forceinline__ G1R g1r_add_lazy_fix(const G1R& p, const G1R& q, const RFp& x3) {
+  if (g1r_is_inf(p)) return q;
+  if (g1r_is_inf(q)) return p;
+  uint32_t z = 0;
+  __asm__ volatile(";; plk rare path" : "+v"(z));
+  RFp x = x3;
+  x.v[0] += z;
+  if (rx_is_zero_u(x)) {
+    G1R d = p;
+    d.X.v[0] += z;
+    d.Y.v[0] += z;
+    return g1r_dbl_lazy(d);
+  }
+  return g1r_infinity();
 }
 
 __device__ __forceinline__ G1R g1r_add_lazy(const G1R& p, const G1R& q) {
   const G1R r = g1r_add_lazy_sl(p, q);
-  if (rx_is_zero(r.ZZ)) {  // rare: an operand at infinity, or equal x (then X3 = R^2 + 6p)
-    if (g1r_is_inf(p)) return q;
-    if (g1r_is_inf(q)) return p;
-    if (rx_is_zero_u(r.X)) return g1r_dbl(g1r_lazy_finish(p));  // R == 0: p == q
-    return g1r_infinity();
-  }
-  return r;
+  return rx_is_zero(r.ZZ) ? g1r_add_lazy_fix(p, q, r.X) : r;  // rare branch
 }
 
 // ---- packed memory <-> limbs (16-byte loads/stores of the 48-byte coordinates) -------

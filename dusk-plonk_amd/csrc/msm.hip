@@ -445,7 +445,17 @@ __global__ void __launch_bounds__(kFine) k_fine(uint32_t B, uint32_t NC, uint32_
   cnt[tid] = 0;
   if (tid < kChunkMax) s_len[tid] = 0;
   __syncthreads();
-  for (uint32_t e = lo + tid; e < hi; e += kFine) atomicAdd(&cnt[in[e].y & (kFine - 1)], 1u);
+  {  // 4 loads in flight per thread, then their atomics
+    uint32_t e = lo + tid;
+    for (; e + 3 * kFine < hi; e += 4 * kFine) {
+      uint32_t k[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) k[u] = in[e + u * kFine].y;
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) atomicAdd(&cnt[k[u] & (kFine - 1)], 1u);
+    }
+    for (; e < hi; e += kFine) atomicAdd(&cnt[in[e].y & (kFine - 1)], 1u);
+  }
   __syncthreads();
   const uint32_t c = cnt[tid];
   if (c % chunk) atomicAdd(&s_len[c % chunk], 1u);
@@ -464,7 +474,18 @@ __global__ void __launch_bounds__(kFine) k_fine(uint32_t B, uint32_t NC, uint32_
   cnt[tid] = v[0];  // cursor of bucket tid, relative to lo
   __syncthreads();
   uint32_t* out = sorted + (size_t)slot * sorted_stride + lo;
-  for (uint32_t e = lo + tid; e < hi; e += kFine) {
+  uint32_t e = lo + tid;
+  for (; e + 3 * kFine < hi; e += 4 * kFine) {
+    uint2 x[4];
+    uint32_t pos[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) x[u] = in[e + u * kFine];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) pos[u] = atomicAdd(&cnt[x[u].y & (kFine - 1)], 1u);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) out[pos[u]] = x[u].x;
+  }
+  for (; e < hi; e += kFine) {
     const uint2 x = in[e];
     out[atomicAdd(&cnt[x.y & (kFine - 1)], 1u)] = x.x;
   }
@@ -615,61 +636,74 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
   }
 }
 
-// Wide bucket sets, reduction step 1: lane r owns the run of K = 2^kRunBits buckets
-// b = rK + t. It forms each bucket sum S_b from the bucket's accumulation partials and keeps
-// running sums from the top of the run, R = sum_t S_(rK+t) and T = sum_t (t + 1) S_(rK+t),
-// then emits Y_r = R and Z_r = T - K R:
+#ifndef PLK_RUNSUM_WAVES
+#define PLK_RUNSUM_WAVES 2  // 256 VGPRs (a few spills) against 271 unconstrained (1 wave per SIMD)
+#endif
+// Wide bucket sets, reduction: runs of K = 2^kRunBits consecutive buckets b = rK + t.
 //   sum_b (b + 1) S_b = sum_r (T_r + rK R_r) = K sum_r (r + 1) Y_r + sum_r Z_r,
+//   R_(r,t) = sum_(t' >= t) S_(rK+t') (suffix sums), Y_r = R_(r,0), T_r = sum_t R_(r,t),
+//   Z_r = T_r - K Y_r.
 // 2 additions per bucket with every lane busy (the bit-sum trees over 2^19 buckets left most
-// lanes idle); the first sum is the bit-sum reduction over the runs, the second a plain sum.
-// The run's tail outside the hot loop (not inlined: one call per 16 buckets): Z = T - K R
-__device__ __noinline__ void runsum_tail(G1R R, G1R T, G1xyzz* __restrict__ z) {
-  for (uint32_t i = 0; i < kRunBits; ++i) R = g1r_dbl(R);
-  st_g1r(z, g1r_lazy_finish(g1r_add_lazy(T, g1r_neg(R))));
-}
-
-__global__ void __launch_bounds__(256) k_runsum(const uint32_t* __restrict__ task_off, uint32_t B,
-                                                uint64_t task_stride,
-                                                const G1xyzz* __restrict__ partials,
-                                                G1xyzz* __restrict__ ys, G1xyzz* __restrict__ zs) {
+// lanes idle); the weighted sum over the runs is the bit-sum reduction, the plain sum of the
+// Z_r an extra output of it. Two kernels with ONE accumulator each (both chains in one lane
+// need 3 live points: over 256 VGPRs).
+//
+// Step 1, lane r: the suffix sums R_(r,t), t = K-1 .. 0, straight from the bucket's
+// accumulation partials (S_b is never formed: R += S_b is the same sum taken partial by
+// partial), stored lazily (X < 8p, Y < 4p fit the packed layout) to rsum[b].
+__global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum1(const uint32_t* __restrict__ task_off, uint32_t B,
+                                                 uint64_t task_stride,
+                                                 const G1xyzz* __restrict__ partials,
+                                                 G1xyzz* __restrict__ rsum) {
   constexpr uint32_t K = 1u << kRunBits;
   const uint32_t slot = blockIdx.y, NR = B >> kRunBits;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= NR) return;
   task_off += (size_t)slot * (B + 1);
   partials += (size_t)slot * task_stride;
-  // One addition per step, operands selected per lane — R += (next partial of the bucket),
-  // or at the bucket's end T += R — so the wave runs ONE inlined addition in lock step
-  // whatever the partial counts of its lanes' buckets (S_b never formed: R += S_b is the
-  // same sum taken partial by partial).
-  G1R R = g1r_infinity(), T = g1r_infinity();
-  uint32_t t = K - 1;
-  uint32_t p = task_off[r * K + t], pe = task_off[r * K + t + 1];  // bucket t's partials
-  for (;;) {
-    const bool part = p < pe;
-    G1R a, b;
-    if (part) {
-      a = R;
-      b = ld_g1r(&partials[p]);
-    } else {
-      a = T;
-      b = R;
-    }
-    const G1R c = g1r_add_lazy(a, b);
-    if (part) {
+  rsum += (size_t)slot * B;
+  // the rare path's copy of the accumulator waits in LDS, not in 56 live registers
+  __shared__ G1xyzz s_prev[256];
+  G1xyzz* prev = &s_prev[threadIdx.x];
+  G1R R = g1r_infinity();
+  uint32_t pe = task_off[r * K + K];
+  for (uint32_t t = K; t-- > 0;) {
+    const uint32_t b = r * K + t;
+    const uint32_t p0 = task_off[b];
+    for (uint32_t p = p0; p < pe; ++p) {
+      st_g1r(prev, R);
+      G1R c = g1r_add_lazy_sl(R, ld_g1r(&partials[p]));
+      if (rx_is_zero(c.ZZ)) c = g1r_add_lazy_fix(ld_g1r(prev), ld_g1r(&partials[p]), c.X);  // rare
       R = c;
-      ++p;
-    } else {
-      T = c;
-      if (t == 0) break;
-      --t;
-      pe = task_off[r * K + t + 1];
-      p = task_off[r * K + t];
     }
+    pe = p0;
+    st_g1r(&rsum[b], R);
   }
-  R = g1r_lazy_finish(R);
-  st_g1r(&ys[(size_t)slot * NR + r], R);
-  runsum_tail(R, T, &zs[(size_t)slot * NR + r]);
+}
+
+// Step 2, lane r: T_r = sum_t R_(r,t), then Y_r = R_(r,0) and Z_r = T_r - K Y_r (canonical
+// [0, 2p) coordinates for the bit sums).
+__global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, const G1xyzz* __restrict__ rsum,
+                                                 G1xyzz* __restrict__ ys, G1xyzz* __restrict__ zs) {
+  constexpr uint32_t K = 1u << kRunBits;
+  const uint32_t slot = blockIdx.y, NR = B >> kRunBits;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= NR) return;
+  rsum += (size_t)slot * B + (size_t)r * K;
+  __shared__ G1xyzz s_prev[256];  // as in k_runsum1
+  G1xyzz* prev = &s_prev[threadIdx.x];
+  G1R T = ld_g1r(&rsum[0]);
+  for (uint32_t t = 1; t < K; ++t) {
+    st_g1r(prev, T);
+    G1R c = g1r_add_lazy_sl(T, ld_g1r(&rsum[t]));
+    if (rx_is_zero(c.ZZ)) c = g1r_add_lazy_fix(ld_g1r(prev), ld_g1r(&rsum[t]), c.X);  // rare
+    T = c;
+  }
+  G1R Y = ld_g1r(&rsum[0]);
+  st_g1r(&ys[(size_t)slot * NR + r], g1r_lazy_finish(Y));
+  for (uint32_t i = 0; i < kRunBits; ++i) Y = g1r_dbl_lazy(Y);
+  Y.Y = rx_sub_u<FpCfg, 3>(rx_zero<FpCfg>(), Y.Y);  // -Y: 3p - Y3 (Y3 < 2p), limbs < 2^30
+  st_g1r(&zs[(size_t)slot * NR + r], g1r_lazy_finish(g1r_add_lazy(T, Y)));
 }
 
 // Bucket reduction sum_b (b+1) S_b, split per workgroup g of 256 buckets b = 256g + u,
@@ -845,6 +879,7 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
     if ((st = w.bin_tot.alloc(slots * 2 * NC * 4))) return st;
     if ((st = w.len_fill.alloc(slots * kChunkMax * 4))) return st;
     if ((st = w.coarse_off.alloc(slots * (NC + 1) * 4))) return st;
+    if ((st = w.rsum.alloc(slots * B * sizeof(G1xyzz)))) return st;
     if ((st = w.ys.alloc(slots * NR * sizeof(G1xyzz)))) return st;
     if ((st = w.zs.alloc(slots * NR * sizeof(G1xyzz)))) return st;
   } else {
@@ -991,9 +1026,11 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     }
   }
   if (wide) {
-    hipLaunchKernelGGL(k_runsum, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream,
+    hipLaunchKernelGGL(k_runsum1, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream,
                        (const uint32_t*)w.task_off.as<uint32_t>(), B, (uint64_t)w.task_stride,
-                       (const G1xyzz*)w.partials.as<G1xyzz>(), w.ys.as<G1xyzz>(), w.zs.as<G1xyzz>());
+                       (const G1xyzz*)w.partials.as<G1xyzz>(), w.rsum.as<G1xyzz>());
+    hipLaunchKernelGGL(k_runsum2, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream, B,
+                       (const G1xyzz*)w.rsum.as<G1xyzz>(), w.ys.as<G1xyzz>(), w.zs.as<G1xyzz>());
   } else {
     // lanes per bucket: until each lane adds ~PLK_LANE_PARTIALS partials (partials per bucket = entries /
     // chunk + 1 tail) or the grid holds 2^17 lanes (the tree levels cost a full addition

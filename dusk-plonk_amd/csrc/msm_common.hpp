@@ -77,7 +77,7 @@ struct MsmWorkspace {
   DevBuf counts, blockhist, offsets, task_off, full_off, len_cur, sorted, tasks, partials, bsum, bits1,
       bits2, flag;
   // wide bucket sets only (msm.hip: two-level sort, run-sum reduction)
-  DevBuf tmp, task_rel, bin_tot, len_fill, coarse_off, ys, zs;
+  DevBuf tmp, task_rel, bin_tot, len_fill, coarse_off, rsum, ys, zs;
   PinnedBuf host_out;  // per-slot bit sums T, flags and entry counts read back by the host
   size_t cap_len = 0, task_stride = 0, sorted_stride = 0;
   uint32_t cap_slots = 0;

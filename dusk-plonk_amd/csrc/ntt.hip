@@ -69,6 +69,87 @@ __device__ __forceinline__ RFr ld_rfr(const Fr* p) { return rx_unpack(ld_fr(p));
 // (ffr.hpp rx_sub_u, R' / r > 70).
 __device__ __forceinline__ RFr sub_u(const RFr& a, const RFr& b) { return rx_sub_u<FrCfg, 3>(a, b); }
 
+// ---- lazy butterfly arithmetic --------------------------------------------------------
+// Between the radix-2 stages (LDS and registers) values keep normalised limbs and a value
+// below 5r instead of [0, 2r): a sum that only feeds the next stage is 9 limb adds, and a
+// normalisation is ONE carry pass that also subtracts q r with q = top limb >> 23 (q r
+// <= value), against the ~70 instructions of a reduced rx_add. R' / r > 70, so every
+// multiplicand below (for canonical twiddles, < r) stays a valid rx_mul operand.
+constexpr uint32_t kB = RxShape<FrCfg>::B;
+constexpr uint32_t kQMax = 32;  // q of a value < 2^260
+
+struct FrLimbTab {
+  uint32_t v[kQMax * kL];
+};
+// row q: the normalised limbs of 2^261 - q r (the top limb's 2^29 is taken off after the add)
+constexpr FrLimbTab make_ztab() {
+  FrLimbTab t{};
+  for (uint32_t q = 0; q < kQMax; ++q) {
+    const RxMultiple<FrCfg> m = rx_multiple<FrCfg>(q, false);  // q r, normalised
+    int64_t br = 0;
+    for (int i = 0; i < kL; ++i) {  // (2^261 - q r) limb by limb
+      const int64_t top = (i == kL - 1) ? (int64_t)1 << kB : 0;
+      int64_t d = top - (int64_t)m.v[i] + br;
+      br = 0;
+      if (i < kL - 1 && d < 0) {
+        d += (int64_t)1 << kB;
+        br = -1;
+      }
+      t.v[q * kL + i] = (uint32_t)d;
+    }
+  }
+  return t;
+}
+__constant__ FrLimbTab kZTab = make_ztab();
+
+// a + c r - b limb by limb, b's limbs below 2^30 - 1 (an unnormalised sum of two normalised
+// values): c r with every limb below the top raised by 2^30 (borrowed from the limb above).
+// Limbs below 2^31.6: rx_mul's columns stay under 2^64 (9 * 2^60.6 + 9 * 2^58).
+template <uint32_t CP>
+struct FrRaised2 {
+  static constexpr RxMultiple<FrCfg> make() {
+    RxMultiple<FrCfg> m = rx_multiple<FrCfg>(CP, false);
+    m.v[0] += 2u << kB;
+    for (int i = 1; i < kL - 1; ++i) m.v[i] += (2u << kB) - 2u;
+    m.v[kL - 1] -= 2u;
+    return m;
+  }
+  static constexpr RxMultiple<FrCfg> k = make();
+};
+template <uint32_t CP>
+__device__ __forceinline__ RFr sub_u2(const RFr& a, const RFr& b) {
+  constexpr RxMultiple<FrCfg> Q = FrRaised2<CP>::k;
+  RFr r;
+#pragma unroll
+  for (int i = 0; i < kL; ++i) r.v[i] = a.v[i] + Q.v[i] - b.v[i];
+  return r;
+}
+
+__device__ __forceinline__ RFr add_u(const RFr& a, const RFr& b) {
+  RFr r;
+#pragma unroll
+  for (int i = 0; i < kL; ++i) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+
+// a (limbs below 2^31, value below 2^260 and >= q r) -> a - q r normalised, q from the
+// unnormalised top limb (low by at most 1): value < (q + 2) 2^255 - q r <= 4r for a < 20r,
+// < 1.6r for a normalised a < 5r (q exact)
+__device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
+  constexpr uint32_t MASK = (1u << kB) - 1;
+  const uint32_t* z = ztab + (a.v[kL - 1] >> (255 - kB * (kL - 1))) * kL;
+  RFr r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < kL - 1; ++i) {
+    const uint32_t t = a.v[i] + z[i] + c;
+    r.v[i] = t & MASK;
+    c = t >> kB;
+  }
+  r.v[kL - 1] = a.v[kL - 1] + z[kL - 1] + c - (1u << kB);
+  return r;
+}
+
 // One Stockham pass. PRE: 0 none, 1 multiply input e by pre[e] (coset g^e).
 // POST: 0 none, 1 multiply by post_scalar, 2 multiply output e by post[e].
 // Data buffers are R-domain (canonical in and out); tw / pre / post / post_scalar are
@@ -95,6 +176,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   const uint32_t TS = PRUNE ? R : H;
   uint32_t* data = smem32;          // kL planes of E
   uint32_t* twl = smem32 + kL * E;
+  uint32_t* ztab = twl + kL * TS;   // kZTab (reduce_q)
 
   // vector blockIdx.y of a batch: its input, output and scale-table rows
   in += (size_t)blockIdx.y * str.in;
@@ -107,6 +189,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   const uint32_t i0 = blockIdx.x << lt;
 
   for (uint32_t x = tid; x < TS; x += bd) lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
+  for (uint32_t x = tid; x < kQMax * kL; x += bd) ztab[x] = kZTab.v[x];
 
   if (PRUNE) {
     __syncthreads();
@@ -170,20 +253,22 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       const uint32_t i2 = ((j + 2 * h) << lt) + t, i3 = ((j + 3 * h) << lt) + t;
       const RFr x0 = lds_ld(data, E, i0), x1 = lds_ld(data, E, i1);
       const RFr x2 = lds_ld(data, E, i2), x3 = lds_ld(data, E, i3);
-      // stage of half 2h: twiddle w^(r s1) for x0/x2 (identity when r = 0), w^((r+h) s1)
-      const RFr y0 = rx_add(x0, x2), y1 = rx_add(x1, x3);
-      const RFr y2 = r != 0 ? rx_mul(sub_u(x0, x2), lds_ld(twl, TS, r << sh1)) : rx_sub(x0, x2);
-      const RFr y3 = rx_mul(sub_u(x1, x3), lds_ld(twl, TS, (r + h) << sh1));
-      // stage of half h: twiddle w^(r s2) for both pairs
-      lds_st(data, E, i0, rx_add(y0, y1));
-      lds_st(data, E, i2, rx_add(y2, y3));
+      // inputs: normalised, < 5r. Stage of half 2h: twiddle w^(r s1) for x0/x2 (identity
+      // when r = 0), w^((r+h) s1) for x1/x3; sums y0, y1 unnormalised (limbs < 2^30, < 10r)
+      const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
+      const RFr y2 = r != 0 ? rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), lds_ld(twl, TS, r << sh1))
+                            : reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 2r / < 4r
+      const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, (r + h) << sh1));
+      // stage of half h: twiddle w^(r s2) for both pairs; outputs normalised, < 5r
+      lds_st(data, E, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
+      lds_st(data, E, i2, reduce_q(add_u(y2, y3), ztab));  // < 6r -> < 4r
       if (r != 0) {
         const RFr w = lds_ld(twl, TS, r << sh2);
-        lds_st(data, E, i1, rx_mul(sub_u(y0, y1), w));
-        lds_st(data, E, i3, rx_mul(sub_u(y2, y3), w));
+        lds_st(data, E, i1, rx_mul(sub_u2<11>(y0, y1), w));         // (y0 - y1 + 11r) w
+        lds_st(data, E, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 4r
       } else {
-        lds_st(data, E, i1, rx_sub(y0, y1));
-        lds_st(data, E, i3, rx_sub(y2, y3));
+        lds_st(data, E, i1, reduce_q(sub_u2<11>(y0, y1), ztab));     // < 21r -> < 4r
+        lds_st(data, E, i3, reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab));
       }
     }
     __syncthreads();
@@ -194,8 +279,8 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       const uint32_t j1 = jb << 1;
       const RFr a = lds_ld(data, E, (j1 << lt) + t);
       const RFr c = lds_ld(data, E, ((j1 + 1) << lt) + t);
-      lds_st(data, E, (j1 << lt) + t, rx_add(a, c));
-      lds_st(data, E, ((j1 + 1) << lt) + t, rx_sub(a, c));
+      lds_st(data, E, (j1 << lt) + t, reduce_q(add_u(a, c), ztab));
+      lds_st(data, E, ((j1 + 1) << lt) + t, reduce_q(rx_sub_u<FrCfg, 6>(a, c), ztab));
     }
     __syncthreads();
   }
@@ -213,9 +298,10 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
     const uint32_t i = i0 + t;
     const uint32_t k = i & (p - 1);
     const size_t pos = ((size_t)(i - k) << lr) + k + ((size_t)m << lp);
-    RFr v = lds_ld(data, E, (bitrev(m, lr) << lt) + t);
+    RFr v = lds_ld(data, E, (bitrev(m, lr) << lt) + t);  // < 5r
     if (POST == 1) v = rx_mul(v, rx_unpack(post_scalar));
-    if (POST == 2) v = rx_mul(v, ld_rfr(&post[pos]));
+    else if (POST == 2) v = rx_mul(v, ld_rfr(&post[pos]));
+    else v = reduce_q(v, ztab);  // < 1.6r
     st_fr(&out[pos], rx_pack_canonical(v));
   }
 }
@@ -405,7 +491,7 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     // zero-padded input (rows j <= R/8 of the first pass only): closed-form first stages
     const bool prune = first && !last && ps.lr >= 4 &&
                        len_in <= ((n >> ps.lr) << (ps.lr - 3)) + (n >> ps.lr);
-    const size_t lds = ((size_t)E + ((1u << ps.lr) >> (prune ? 0 : 1))) * kL * sizeof(uint32_t);
+    const size_t lds = ((size_t)E + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) * kL * sizeof(uint32_t);
     dim3 grid(blocks, count);
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
