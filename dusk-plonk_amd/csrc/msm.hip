@@ -637,16 +637,15 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
 }
 
 #ifndef PLK_RUNSUM_WAVES
-#define PLK_RUNSUM_WAVES 2  // 256 VGPRs (a few spills) against 271 unconstrained (1 wave per SIMD)
+#define PLK_RUNSUM_WAVES 1  // ~270 VGPRs; a 2-wave cap spills in the loop (runsum1 3.43 -> 3.07 ms per proof uncapped)
 #endif
 // Wide bucket sets, reduction: runs of K = 2^kRunBits consecutive buckets b = rK + t.
-//   sum_b (b + 1) S_b = sum_r (T_r + rK R_r) = K sum_r (r + 1) Y_r + sum_r Z_r,
-//   R_(r,t) = sum_(t' >= t) S_(rK+t') (suffix sums), Y_r = R_(r,0), T_r = sum_t R_(r,t),
-//   Z_r = T_r - K Y_r.
+//   sum_b (b + 1) S_b = sum_r (T_r + rK Y_r) = K (sum_r (r + 1) Y_r - sum_r Y_r) + sum_r T_r,
+//   R_(r,t) = sum_(t' >= t) S_(rK+t') (suffix sums), Y_r = R_(r,0), T_r = sum_t R_(r,t).
 // 2 additions per bucket with every lane busy (the bit-sum trees over 2^19 buckets left most
-// lanes idle); the weighted sum over the runs is the bit-sum reduction, the plain sum of the
-// Z_r an extra output of it. Two kernels with ONE accumulator each (both chains in one lane
-// need 3 live points: over 256 VGPRs).
+// lanes idle); the weighted sum over the runs is the bit-sum reduction, sum_r Y_r (its A)
+// and sum_r T_r extra outputs of it, the host multiplies by K. Two kernels with ONE
+// accumulator each (both chains in one lane need 3 live points: over 256 VGPRs).
 //
 // Step 1, lane r: the suffix sums R_(r,t), t = K-1 .. 0, straight from the bucket's
 // accumulation partials (S_b is never formed: R += S_b is the same sum taken partial by
@@ -681,10 +680,10 @@ __global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum1(const uint32_
   }
 }
 
-// Step 2, lane r: T_r = sum_t R_(r,t), then Y_r = R_(r,0) and Z_r = T_r - K Y_r (canonical
-// [0, 2p) coordinates for the bit sums).
+// Step 2, lane r: T_r = sum_t R_(r,t) and Y_r = R_(r,0) (canonical [0, 2p) coordinates for
+// the bit sums).
 __global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, const G1xyzz* __restrict__ rsum,
-                                                 G1xyzz* __restrict__ ys, G1xyzz* __restrict__ zs) {
+                                                 G1xyzz* __restrict__ ys, G1xyzz* __restrict__ ts) {
   constexpr uint32_t K = 1u << kRunBits;
   const uint32_t slot = blockIdx.y, NR = B >> kRunBits;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -699,11 +698,8 @@ __global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, c
     if (rx_is_zero(c.ZZ)) c = g1r_add_lazy_fix(ld_g1r(prev), ld_g1r(&rsum[t]), c.X);  // rare
     T = c;
   }
-  G1R Y = ld_g1r(&rsum[0]);
-  st_g1r(&ys[(size_t)slot * NR + r], g1r_lazy_finish(Y));
-  for (uint32_t i = 0; i < kRunBits; ++i) Y = g1r_dbl_lazy(Y);
-  Y.Y = rx_sub_u<FpCfg, 3>(rx_zero<FpCfg>(), Y.Y);  // -Y: 3p - Y3 (Y3 < 2p), limbs < 2^30
-  st_g1r(&zs[(size_t)slot * NR + r], g1r_lazy_finish(g1r_add_lazy(T, Y)));
+  st_g1r(&ys[(size_t)slot * NR + r], g1r_lazy_finish(ld_g1r(&rsum[0])));
+  st_g1r(&ts[(size_t)slot * NR + r], g1r_lazy_finish(T));
 }
 
 // Bucket reduction sum_b (b+1) S_b, split per workgroup g of 256 buckets b = 256g + u,
@@ -725,22 +721,28 @@ __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
   return ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
 }
 
-__global__ void __launch_bounds__(256) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
-                                                 const G1xyzz* __restrict__ zin,
-                                                 G1xyzz* __restrict__ out) {
-  __shared__ G1xyzz sh[256 + 32];  // [0, 256): buckets, then tree partials; [256, 288): rows, columns
+template <bool Z>
+__global__ void __launch_bounds__(Z ? 384 : 256) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
+                                                           const G1xyzz* __restrict__ zin,
+                                                           G1xyzz* __restrict__ out) {
+  // [0, NV): the group's values (buckets or run sums Y; with Z also the 256 plain-sum values),
+  // [NV, NV + NS): row / column sums (and the 16 row sums of the plain-sum values)
+  constexpr uint32_t NV = Z ? 512 : 256, NS = Z ? 48 : 32;
+  __shared__ G1xyzz sh[NV + NS];
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
   out += ((size_t)slot * gridDim.x + g) * kBitsumOut;
-  {
-    const uint32_t b = g * 256 + tid;
-    if (b < B) sh[tid] = bsum[(size_t)slot * B + b];
-    else st_g1r(&sh[tid], g1r_infinity());
+  for (uint32_t x = tid; x < NV; x += blockDim.x) {
+    const uint32_t b = g * 256 + (x & 255);
+    const G1xyzz* src = x < 256 ? bsum : zin;
+    if (b < B) sh[x] = src[(size_t)slot * B + b];
+    else st_g1r(&sh[x], g1r_infinity());
   }
   __syncthreads();
-  {  // sum q < 16: row a = q; q >= 16: column c = q - 16. Lane e of its 8 adds members 2e, 2e + 1.
+  {  // sum q < 16: row a = q; 16 <= q < 32: column c = q - 16; q >= 32 (Z): row q - 32 of the
+     // plain-sum values. Lane e of its 8 adds members 2e, 2e + 1.
     const uint32_t q = tid >> 3, e = tid & 7;
-    const uint32_t m0 = q < 16 ? 16 * q + 2 * e : (q - 16) + 32 * e;
-    const uint32_t m1 = q < 16 ? m0 + 1 : m0 + 16;
+    const uint32_t m0 = q < 16 ? 16 * q + 2 * e : q < 32 ? (q - 16) + 32 * e : 256 + 16 * (q - 32) + 2 * e;
+    const uint32_t m1 = (q >= 16 && q < 32) ? m0 + 16 : m0 + 1;
     const G1R acc = g1r_add(ld_g1r(&sh[m0]), ld_g1r(&sh[m1]));
     __syncthreads();
     st_g1r(&sh[tid], acc);
@@ -749,23 +751,23 @@ __global__ void __launch_bounds__(256) k_bitsum1(uint32_t B, const G1xyzz* __res
       if (e < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
       __syncthreads();
     }
-    if (e == 0) sh[256 + q] = sh[tid];
+    if (e == 0) sh[NV + q] = sh[tid];
     __syncthreads();
   }
   // wave 0: lanes 0..31 = T_0..T_7, 4 lanes each (2 terms per lane); lanes 32..39 = A_g, 8 lanes
-  // (rows 2e, 2e + 1); then trees
-  if (tid < 40) {
-    const uint32_t s = tid < 32 ? tid >> 2 : 8, e = tid < 32 ? tid & 3 : tid - 32;
+  // (rows 2e, 2e + 1); with Z lanes 40..47 = the plain sum (its rows 2e, 2e + 1); then trees
+  if (tid < (Z ? 48u : 40u)) {
+    const uint32_t s = tid < 32 ? tid >> 2 : tid < 40 ? 8 : 9, e = tid < 32 ? tid & 3 : (tid - 32) & 7;
     const uint32_t w = tid < 32 ? 4 : 8;
     uint32_t i0, i1;
     if (s < 4) {  // columns c with bit s
-      i0 = 256 + 16 + with_bit(2 * e, s);
-      i1 = 256 + 16 + with_bit(2 * e + 1, s);
+      i0 = NV + 16 + with_bit(2 * e, s);
+      i1 = NV + 16 + with_bit(2 * e + 1, s);
     } else if (s < 8) {  // rows a with bit s - 4
-      i0 = 256 + with_bit(2 * e, s - 4);
-      i1 = 256 + with_bit(2 * e + 1, s - 4);
-    } else {
-      i0 = 256 + 2 * e;
+      i0 = NV + with_bit(2 * e, s - 4);
+      i1 = NV + with_bit(2 * e + 1, s - 4);
+    } else {  // all rows (A_g) / all plain-sum rows
+      i0 = NV + (s == 8 ? 0 : 32) + 2 * e;
       i1 = i0 + 1;
     }
     st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[i0]), ld_g1r(&sh[i1])));
@@ -780,22 +782,11 @@ __global__ void __launch_bounds__(256) k_bitsum1(uint32_t B, const G1xyzz* __res
     }
     if (e == 0) out[s] = sh[tid];
   }
-  if (zin) {  // plain tree sum of the group's Z values
-    __syncthreads();
-    const uint32_t b = g * 256 + tid;
-    if (b < B) sh[tid] = zin[(size_t)slot * B + b];
-    else st_g1r(&sh[tid], g1r_infinity());
-    __syncthreads();
-    for (uint32_t h = 128; h >= 1; h >>= 1) {
-      if (tid < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
-      __syncthreads();
-    }
-    if (tid == 0) out[9] = sh[0];
-  }
 }
 
 // Workgroup j of slot: T_j = sum_g T_j(g) for 0 < j < 8; T_0 = sum_g (T_0(g) + A_g);
-// T_(8+i) = sum_(g: bit i of g) A_g; j = nbits (wide bucket sets): sum_g Z_g.
+// T_(8+i) = sum_(g: bit i of g) A_g; wide bucket sets: j = nbits sum_g of the plain sums,
+// j = nbits + 1 sum_g A_g.
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, uint32_t nout,
                                                  G1xyzz* __restrict__ out) {
@@ -805,8 +796,8 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
   G1R acc = g1r_infinity();
   for (uint32_t g = tid; g < G; g += 256) {
     const G1xyzz* e = &in[(size_t)g * kBitsumOut];
-    if (j == nbits) {
-      acc = g1r_add(acc, ld_g1r(&e[9]));
+    if (j >= nbits) {  // wide sets: sum_g of the plain sums (j = nbits) and of A_g (nbits + 1)
+      acc = g1r_add(acc, ld_g1r(&e[j == nbits ? 9 : 8]));
     } else if (j < 8) {
       acc = g1r_add(acc, ld_g1r(&e[j]));
       if (j == 0) acc = g1r_add(acc, ld_g1r(&e[8]));
@@ -933,7 +924,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   const uint32_t NC = B >> kFineBits, NR = B >> kRunBits;
   const uint32_t G = cdiv(wide ? NR : B, 256);  // a power of two
   const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
-  const uint32_t nout = nbits + (wide ? 1u : 0u);         // + the plain sum of the Z values
+  const uint32_t nout = nbits + (wide ? 2u : 0u);         // + sum_r T_r, sum_r Y_r
   const uint32_t slots = (uint32_t)count;
   // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads; wide
   // sets have few entries per bucket and enough tasks anyway: one task per bucket
@@ -1042,9 +1033,15 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
                        w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
   }
-  hipLaunchKernelGGL(k_bitsum1, dim3(G, slots), dim3(256), 0, stream, wide ? NR : B,
-                     (const G1xyzz*)(wide ? w.ys.as<G1xyzz>() : w.bsum.as<G1xyzz>()),
-                     (const G1xyzz*)(wide ? w.zs.as<G1xyzz>() : nullptr), w.bits1.as<G1xyzz>());
+  if (wide) {
+    hipLaunchKernelGGL(k_bitsum1<true>, dim3(G, slots), dim3(384), 0, stream, NR,
+                       (const G1xyzz*)w.ys.as<G1xyzz>(), (const G1xyzz*)w.zs.as<G1xyzz>(),
+                       w.bits1.as<G1xyzz>());
+  } else {
+    hipLaunchKernelGGL(k_bitsum1<false>, dim3(G, slots), dim3(256), 0, stream, B,
+                       (const G1xyzz*)w.bsum.as<G1xyzz>(), (const G1xyzz*)nullptr,
+                       w.bits1.as<G1xyzz>());
+  }
   hipLaunchKernelGGL(k_bitsum2, dim3(nout, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
                      G, nbits, nout, w.bits2.as<G1xyzz>());
   PLK_HIP_TRY(hipGetLastError());
@@ -1087,7 +1084,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
       acc = xyzz_dbl(acc);
       acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + j]));
     }
-    if (wide) {  // sum over the runs: K * sum_r (r + 1) Y_r + sum_r Z_r (k_runsum)
+    if (wide) {  // over the runs: K (sum_r (r + 1) Y_r - sum_r Y_r) + sum_r T_r (k_runsum2)
+      G1xyzz a = rx_to_r_domain(T[(size_t)k * nout + nbits + 1]);
+      a.Y = fe_neg(a.Y);
+      acc = xyzz_add(acc, a);
       for (uint32_t i = 0; i < kRunBits; ++i) acc = xyzz_dbl(acc);
       acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + nbits]));
     }

@@ -107,15 +107,18 @@ static uint32_t choose_c(size_t n) {
 #define PLK_C_HUGE 20
 #endif
   if (n >= (1u << 20)) return PLK_C_HUGE;
-  // c = 17: 15 windows of the half-range scalars (msm.hip scalar_half) against 16 at c = 16
+  // 2^16 .. 2^20 points: c = 17, 15 windows of exactly 255 bits (no short top window), 2^16
+  // buckets through the wide-set path. 2^16 bench (tools/gpu_c_sweep.sh, same box, twice):
+  // c = 15 20.3 / 20.3, 16 18.9 / 18.3, 17 20.7 / 21.1 M constraints/s; c = 18 (and 19 at 2^20)
+  // collapse to 8.4 (17.6) M: their top windows hold 2 (7) bits, so every scalar's top digit
+  // lands in one of 4 (128) buckets of 2^16 (8 192) entries each, summed by single lanes
 #ifndef PLK_C_LARGE
-#define PLK_C_LARGE 16  // 17 (15 windows) measured slower end to end: its 2x buckets cost more in the sort and reduction kernels than the 6% fewer entries save
+#define PLK_C_LARGE 17
 #endif
-  if (n >= (1u << 18)) return PLK_C_LARGE;
-// 2^14 .. 2^17 points: c = 15 (17 windows, top window 14 bits) against 13 (20 windows):
-// 2^16 bench 18.3 -> 19.4 M constraints/s (same box, two repetitions each,
-// tools/gpu_ab_c.sh); c = 16 is slower there (17.8 M: its 8x buckets against 20 % fewer
-// entries), and c = 14 leaves a 2-bit top window (a few huge buckets)
+  if (n >= (1u << 16)) return PLK_C_LARGE;
+// 2^14 .. 2^15 points: c = 15 (17 windows, top window 14 bits) against 13 (20 windows):
+// 2^16 bench 18.3 -> 19.4 M constraints/s in round 1 (tools/gpu_ab_c.sh); c = 14 leaves a
+// 2-bit top window (a few huge buckets)
 #ifndef PLK_C_MID
 #define PLK_C_MID 15
 #endif

@@ -56,7 +56,8 @@ def test_msm_vs_oracle(plk, gpu_ctx, oracle, logn):
     tau = random_fr(1, seed=logn)[0]
     pp = plk.PlonkParams.setup(logn, tau, gpu_ctx, n_points=n + 8)
     pts = pp.points()
-    # logn = 18: the c = 17 / 15-window configuration of n >= 2^18 (srs.hip choose_c)
+    # logn = 16, 18: c = 17 (15 windows, 2^16 buckets: the wide-set sort and run-sum
+    # reduction of msm.hip); below 2^16 the LDS-histogram path (srs.hip choose_c)
     if logn <= 12:  # the SRS itself against the oracle's setup
         assert np.array_equal(pts, oracle.srs(tau, n + 8))
     sc = random_fr(n, seed=1000 + logn)
