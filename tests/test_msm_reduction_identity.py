@@ -1,0 +1,87 @@
+"""CPU check of the bucket-reduction identities the MSM kernels rely on (msm.hip), with
+integers standing in for the bucket sums (the identities are linear, so any abelian group
+behaves the same):
+
+* run-sum form (wide bucket sets, k_runsum1/2 + k_bitsum1/2 + host tail):
+  sum_b (b+1) S_b = K (sum_r (r+1) Y_r - sum_r Y_r) + sum_r T_r, runs of K buckets,
+  Y_r = R_(r,0), T_r = sum_t R_(r,t), R_(r,t) = sum_(t'>=t) S_(rK+t');
+* bit-sum form (k_bitsum1/2): sum_u (u+1) S_u = sum_j 2^j T_j with b = 256 g + 16 a + c,
+  T_j(g) from row / column sums and the group term (256 g + 1) A_g spread over T_(8+i);
+* the top-window-free recoding: signed c-bit digits of a scalar below 2^254 reconstruct it
+  with W = ceil(255 / c) windows and never exceed 2^(c-1) (msm.hip digit_at).
+"""
+import random
+
+import pytest
+
+
+def weighted(S):
+    return sum((b + 1) * s for b, s in enumerate(S))
+
+
+@pytest.mark.parametrize("K,nruns", [(16, 8), (16, 33), (4, 5)])
+def test_run_sum_identity(K, nruns):
+    rng = random.Random(K * 1000 + nruns)
+    S = [rng.randrange(-10**6, 10**6) if rng.random() > 0.1 else 0 for _ in range(K * nruns)]
+    Y, T = [], []
+    for r in range(nruns):
+        suffix = [sum(S[r * K + t2] for t2 in range(t, K)) for t in range(K)]
+        Y.append(suffix[0])
+        T.append(sum(suffix))
+    assert weighted(S) == K * (weighted(Y) - sum(Y)) + sum(T)
+
+
+def bitsum_device(S):
+    """k_bitsum1 (per group of 256: rows / columns -> T_j(g), A_g) and k_bitsum2."""
+    B = len(S)
+    G = (B + 255) // 256
+    nbits = 8 + (G - 1).bit_length() if G > 1 else 8
+    out = []
+    for g in range(G):
+        sg = [S[256 * g + u] if 256 * g + u < B else 0 for u in range(256)]
+        row = [sum(sg[16 * a + c] for c in range(16)) for a in range(16)]
+        col = [sum(sg[16 * a + c] for a in range(16)) for c in range(16)]
+        t = [sum(col[c] for c in range(16) if (c >> j) & 1) for j in range(4)]
+        t += [sum(row[a] for a in range(16) if (a >> i) & 1) for i in range(4)]
+        out.append((t, sum(row)))
+    T = []
+    for j in range(nbits):
+        if j < 8:
+            T.append(sum(o[0][j] for o in out) + (sum(o[1] for o in out) if j == 0 else 0))
+        else:
+            T.append(sum(o[1] for g, o in enumerate(out) if (g >> (j - 8)) & 1))
+    return sum((1 << j) * T[j] for j in range(nbits))
+
+
+@pytest.mark.parametrize("B", [256, 1024, 4096])
+def test_bitsum_identity(B):
+    rng = random.Random(B)
+    S = [rng.randrange(-10**6, 10**6) for _ in range(B)]
+    assert bitsum_device(S) == weighted(S)
+
+
+def digits(s, c, W):
+    """msm.hip digit_at over all windows (carry threaded)."""
+    out, carry = [], 0
+    for w in range(W):
+        val = (s >> (w * c)) & ((1 << c) - 1) if w * c < 256 else 0
+        d = val + carry
+        if d > (1 << (c - 1)):
+            d -= 1 << c
+            carry = 1
+        else:
+            carry = 0
+        out.append(d)
+    return out, carry
+
+
+@pytest.mark.parametrize("c", [8, 10, 13, 15, 16, 17, 20])
+def test_signed_recoding(c):
+    W = (255 + c - 1) // c
+    rng = random.Random(c)
+    cases = [0, 1, (1 << 254) - 1, (1 << 253) + 12345] + [rng.randrange(1 << 254) for _ in range(200)]
+    for s in cases:
+        d, carry = digits(s, c, W)
+        assert carry == 0
+        assert all(abs(x) <= 1 << (c - 1) for x in d)
+        assert sum(x << (w * c) for w, x in enumerate(d)) == s
