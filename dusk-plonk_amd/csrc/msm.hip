@@ -306,7 +306,10 @@ __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
 constexpr uint32_t kFineBits = 10;
 constexpr uint32_t kFine = 1u << kFineBits;  // buckets per coarse bin = threads of k_fine
 constexpr uint32_t kCoarseMax = 4096;        // coarse bins (B <= 2^22, c <= 23)
-constexpr uint32_t kRunBits = 4;             // bucket reduction: runs of 16 buckets per lane
+// bucket reduction: runs of 2^rb buckets per lane, rb = kRunBits (16) for batches of several
+// MSMs; a lone MSM takes kRunBitsLone (8): twice the lanes, half the chain per lane (its
+// run-sum kernels are latency-bound on half the chip otherwise)
+constexpr uint32_t kRunBits = 4, kRunBitsLone = 3;
 
 // Exclusive scan over the workgroup of K values per thread (wave shuffles, then the wave
 // totals through LDS); tot = the workgroup totals. sh: K * 32 words.
@@ -639,7 +642,7 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
 #ifndef PLK_RUNSUM_WAVES
 #define PLK_RUNSUM_WAVES 1  // ~270 VGPRs; a 2-wave cap spills in the loop (runsum1 3.43 -> 3.07 ms per proof uncapped)
 #endif
-// Wide bucket sets, reduction: runs of K = 2^kRunBits consecutive buckets b = rK + t.
+// Wide bucket sets, reduction: runs of K = 2^rb consecutive buckets b = rK + t.
 //   sum_b (b + 1) S_b = sum_r (T_r + rK Y_r) = K (sum_r (r + 1) Y_r - sum_r Y_r) + sum_r T_r,
 //   R_(r,t) = sum_(t' >= t) S_(rK+t') (suffix sums), Y_r = R_(r,0), T_r = sum_t R_(r,t).
 // 2 additions per bucket with every lane busy (the bit-sum trees over 2^19 buckets left most
@@ -650,12 +653,12 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
 // Step 1, lane r: the suffix sums R_(r,t), t = K-1 .. 0, straight from the bucket's
 // accumulation partials (S_b is never formed: R += S_b is the same sum taken partial by
 // partial), stored lazily (X < 8p, Y < 4p fit the packed layout) to rsum[b].
-__global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum1(const uint32_t* __restrict__ task_off, uint32_t B,
+__global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum1(const uint32_t* __restrict__ task_off, uint32_t B, uint32_t rb,
                                                  uint64_t task_stride,
                                                  const G1xyzz* __restrict__ partials,
                                                  G1xyzz* __restrict__ rsum) {
-  constexpr uint32_t K = 1u << kRunBits;
-  const uint32_t slot = blockIdx.y, NR = B >> kRunBits;
+  const uint32_t K = 1u << rb;
+  const uint32_t slot = blockIdx.y, NR = B >> rb;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= NR) return;
   task_off += (size_t)slot * (B + 1);
@@ -682,10 +685,10 @@ __global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum1(const uint32_
 
 // Step 2, lane r: T_r = sum_t R_(r,t) and Y_r = R_(r,0) (canonical [0, 2p) coordinates for
 // the bit sums).
-__global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, const G1xyzz* __restrict__ rsum,
+__global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, uint32_t rb, const G1xyzz* __restrict__ rsum,
                                                  G1xyzz* __restrict__ ys, G1xyzz* __restrict__ ts) {
-  constexpr uint32_t K = 1u << kRunBits;
-  const uint32_t slot = blockIdx.y, NR = B >> kRunBits;
+  const uint32_t K = 1u << rb;
+  const uint32_t slot = blockIdx.y, NR = B >> rb;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= NR) return;
   rsum += (size_t)slot * B + (size_t)r * K;
@@ -847,7 +850,7 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
   slots = std::max(slots, w.cap_slots);
   const size_t B = (size_t)1 << (s->c - 1);
   const bool wide = B > kLdsBuckets;
-  const size_t NC = B >> kFineBits, NR = B >> kRunBits;
+  const size_t NC = B >> kFineBits, NR = B >> kRunBitsLone;  // the most runs
   if (wide && NC > kCoarseMax) return PLK_E_ARG;
   const size_t entries = (size_t)s->windows * len;
   const size_t max_tasks = entries / kChunkMin + B + 1;
@@ -919,9 +922,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1)};
   const uint32_t B = cfg.B;
   // wide bucket sets: two-level sort and run-sum reduction; the bit sums then run over the
-  // NR = B / 2^kRunBits runs instead of the buckets
+  // NR = B / 2^rb runs instead of the buckets
   const bool wide = B > kLdsBuckets;
-  const uint32_t NC = B >> kFineBits, NR = B >> kRunBits;
+  const uint32_t rb = count == 1 ? kRunBitsLone : kRunBits;
+  const uint32_t NC = B >> kFineBits, NR = B >> rb;
   const uint32_t G = cdiv(wide ? NR : B, 256);  // a power of two
   const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
   const uint32_t nout = nbits + (wide ? 2u : 0u);         // + sum_r T_r, sum_r Y_r
@@ -1018,9 +1022,9 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   }
   if (wide) {
     hipLaunchKernelGGL(k_runsum1, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream,
-                       (const uint32_t*)w.task_off.as<uint32_t>(), B, (uint64_t)w.task_stride,
+                       (const uint32_t*)w.task_off.as<uint32_t>(), B, rb, (uint64_t)w.task_stride,
                        (const G1xyzz*)w.partials.as<G1xyzz>(), w.rsum.as<G1xyzz>());
-    hipLaunchKernelGGL(k_runsum2, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream, B,
+    hipLaunchKernelGGL(k_runsum2, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream, B, rb,
                        (const G1xyzz*)w.rsum.as<G1xyzz>(), w.ys.as<G1xyzz>(), w.zs.as<G1xyzz>());
   } else {
     // lanes per bucket: until each lane adds ~PLK_LANE_PARTIALS partials (partials per bucket = entries /
@@ -1088,7 +1092,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
       G1xyzz a = rx_to_r_domain(T[(size_t)k * nout + nbits + 1]);
       a.Y = fe_neg(a.Y);
       acc = xyzz_add(acc, a);
-      for (uint32_t i = 0; i < kRunBits; ++i) acc = xyzz_dbl(acc);
+      for (uint32_t i = 0; i < rb; ++i) acc = xyzz_dbl(acc);
       acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + nbits]));
     }
     Fp x, y;
