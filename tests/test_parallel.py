@@ -213,6 +213,14 @@ def test_sharded_prover_two_ranks_one_gpu(plk, gpu_ctx):
 
 
 @pytest.mark.gpu
+def test_sharded_prover_two_ranks_wide_slices(plk, gpu_ctx):
+    """2^17: each rank's SRS slice holds over 2^16 points, so the sharded commits run the
+    MSM's wide-bucket path (c = 17: two-level sort, run-sum reduction) on every rank."""
+    out = _spawn(_sharded_prover_worker, 2, 17)
+    assert out == {0: True, 1: True}
+
+
+@pytest.mark.gpu
 def test_sharded_prover_three_ranks_uneven(plk, gpu_ctx):
     out = _spawn(_sharded_prover_worker, 3, 10)
     assert out == {0: True, 1: True, 2: True}
