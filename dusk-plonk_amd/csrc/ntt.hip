@@ -54,14 +54,24 @@ constexpr int kL = RxShape<FrCfg>::L;
 // plane for a run-time stride.
 constexpr uint32_t kDS = 1u << kMaxLe;
 
+// Element idx of a data plane sits at word idx ^ ((idx / 32) * 9 mod 32): ds_read_b32 /
+// ds_write_b32 bank by word mod 32 per 32-lane half, and the unswizzled columns put the
+// bit-reversed output reads on one bank (32-way at the first pass of 2^20 / 2^23: ~15 us of a
+// 2^20 transform) and some radix-4 rows on 2 - 4. With the swizzle every 2^20 pass is
+// conflict-free and 2^23 keeps 64 extra cycles per workgroup in ~3 000 (bank model over the
+// kernel's index patterns, sizes 2^12 .. 2^23). A permutation of the low 5 bits: stays in [0, E).
+__device__ __forceinline__ uint32_t swz(uint32_t idx) { return idx ^ (((idx >> 5) * 9u) & 31u); }
+
 __device__ __forceinline__ RFr lds_ldd(const uint32_t* base, uint32_t idx) {
   RFr r;
+  idx = swz(idx);
 #pragma unroll
   for (int l = 0; l < kL; ++l) r.v[l] = base[l * kDS + idx];
   return r;
 }
 
 __device__ __forceinline__ void lds_std(uint32_t* base, uint32_t idx, const RFr& v) {
+  idx = swz(idx);
 #pragma unroll
   for (int l = 0; l < kL; ++l) base[l * kDS + idx] = v.v[l];
 }
@@ -236,21 +246,47 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       }
     }
   }
-  for (uint32_t e = tid; e < (PRUNE ? 0u : E); e += bd) {
-    const uint32_t t = e & (T - 1), j = e >> lt;
-    const uint32_t i = i0 + t;
-    const size_t g = (size_t)i + ((size_t)j << nr_log);
-    RFr v;
-    if (g < len_in) {
-      v = ld_rfr(&in[g]);
-      if (PRE == 1) v = rx_mul(v, ld_rfr(&pre[g]));
-    } else {
-      v = rx_zero<FrCfg>();
+  if (!PRUNE) {
+    // every load of the thread's (at most kLoadIt, E / bd <= 4) elements is issued before the
+    // first multiply: one HBM latency per pass instead of one per element
+    // The loads are unconditional (clamped indices; the host passes a valid `in` even for
+    // len_in = 0) and zero-padding is a select afterwards: a conditional load would merge
+    // with its alternative at a join and wait there.
+    constexpr uint32_t kLoadIt = 4;
+    const uint32_t nit = (E + bd - 1) / bd;  // uniform, <= kLoadIt
+    Fr raw[kLoadIt], aux[kLoadIt];           // input; coset factor (PRE) or inter-pass twiddle
+#pragma unroll
+    for (uint32_t c = 0; c < kLoadIt; ++c) {  // all kLoadIt (duplicates past E / bd)
+      const uint32_t e = min(tid + c * bd, E - 1);
+      const size_t g = (size_t)(i0 + (e & (T - 1))) + ((size_t)(e >> lt) << nr_log);
+      const size_t gc = g < len_in ? g : 0;
+      raw[c] = ld_fr(&in[gc]);
+      if (PRE == 1) aux[c] = ld_fr(&pre[gc]);
     }
-    const uint32_t k = i & (p - 1);
-    // inter-pass twiddle w_{Rp}^{jk} from the pass table laid out [j][k] (coalesced in k)
-    if (j != 0 && k != 0) v = rx_mul(v, ld_rfr(&ptw[((size_t)j << lp) + k]));
-    lds_std(data, (j << lt) + t, v);
+    // inter-pass twiddle w_{Rp}^{jk} from the pass table laid out [j][k] (coalesced in k);
+    // every (j, k) is in the table, the j = 0 / k = 0 entries are skipped below
+    if (PRE != 1 && lp != 0) {
+#pragma unroll
+      for (uint32_t c = 0; c < kLoadIt; ++c) {
+        const uint32_t e = min(tid + c * bd, E - 1);
+        aux[c] = ld_fr(&ptw[((size_t)(e >> lt) << lp) + ((i0 + (e & (T - 1))) & (p - 1))]);
+      }
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < kLoadIt; ++c) {
+      if (c >= nit) break;
+      const uint32_t e = tid + c * bd;
+      const uint32_t t = e & (T - 1), j = e >> lt;
+      const uint32_t i = i0 + t;
+      const size_t g = (size_t)i + ((size_t)j << nr_log);
+      RFr v = rx_zero<FrCfg>();
+      if (g < len_in) {
+        v = rx_unpack(raw[c]);
+        if (PRE == 1) v = rx_mul(v, rx_unpack(aux[c]));
+      }
+      if (PRE != 1 && lp != 0 && j != 0 && (i & (p - 1)) != 0) v = rx_mul(v, rx_unpack(aux[c]));
+      if (e < E) lds_std(data, (j << lt) + t, v);
+    }
   }
   __syncthreads();
 
@@ -492,7 +528,9 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
   Fr* s2 = scratch + n * count;
   const Fr* tw = dir > 0 ? d->tw_fwd_rx.as<Fr>() : d->tw_inv.as<Fr>();
   const Fr n_inv_rx = fe_to_rx_domain(d->n_inv);
-  const Fr* src = in;
+  // an all-zero input still has its (clamped, discarded) loads: point them at a live table
+  const bool no_input = len_in == 0;
+  const Fr* src = no_input ? tw : in;
   for (size_t q = 0; q < P; ++q) {
     const NttPass& ps = d->plan[q];
     Fr* dst = (q + 1 == P) ? out : ((q & 1) ? s2 : s1);
@@ -513,7 +551,7 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
     NttStrides str;
-    str.in = first ? bt.in_stride : n * 1;
+    str.in = first ? (no_input ? 0 : bt.in_stride) : n * 1;
     str.out = last ? bt.out_stride : n * 1;
     str.pre = bt.pre ? bt.pre_stride : 0;
     str.post = bt.post ? bt.post_stride : 0;
