@@ -39,7 +39,7 @@ namespace plk {
 namespace {
 
 #ifndef PLK_LANE_PARTIALS
-#define PLK_LANE_PARTIALS 8  // bucket partials per k_bucket_sum lane aimed at (4: +0.1 ms per proof)
+#define PLK_LANE_PARTIALS 4  // bucket partials per k_bucket_sum lane aimed at (only c <= 15, SRS < 2^16: 8 -> 4 gave 2^12 3.74 -> 3.93 M constraints/s, tools/gpu_ab_quick.sh)
 #endif
 #ifndef PLK_CHUNK_TARGET
 #define PLK_CHUNK_TARGET 262144  // accumulation tasks aimed at per batch (chunk = entries / this)
@@ -610,14 +610,23 @@ __global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* 
 }
 
 // Bucket sums S_b = sum of bucket b's accumulation partials (task_off[b] .. task_off[b+1]):
-// 2^lp lanes per bucket, each adding every 2^lp-th partial, then an LDS tree over the lanes
-// (2^lp is sized on the host to the partials per bucket, so the sequential chain stays
-// ~PLK_LANE_PARTIALS additions at every MSM size, unless the grid is already full).
+// 2^lp lanes per bucket (consecutive lanes of one wave, 2^lp <= 16), each adding every
+// 2^lp-th partial, then a tree over the lanes through cross-lane shuffles of the packed
+// point (no LDS: these long add chains would otherwise hold 48 KiB of a CU's LDS per
+// workgroup while other proofs' kernels wait for it). 2^lp is sized on the host to the
+// partials per bucket, so the sequential chain stays ~PLK_LANE_PARTIALS additions at every
+// MSM size, unless the grid is already full.
+__device__ __forceinline__ RFp shfl_down_rfp(const RFp& v, uint32_t h) {
+  Fp x = rx_pack(v);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x.v[i] = __shfl_down(x.v[i], h, 64);
+  return rx_unpack(x);
+}
+
 __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__ task_off,
                                                     uint32_t B, uint32_t lp, uint64_t task_stride,
                                                     const G1xyzz* __restrict__ partials,
                                                     G1xyzz* __restrict__ bsum) {
-  __shared__ G1xyzz sh[256];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x;
   const uint32_t P = 1u << lp, s = tid & (P - 1);
   const uint32_t b = (blockIdx.x * 256 + tid) >> lp;
@@ -626,17 +635,15 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
   G1R acc = g1r_infinity();
   if (b < B)
     for (uint32_t t = task_off[b] + s; t < task_off[b + 1]; t += P) acc = g1r_add(acc, ld_g1r(&partials[t]));
-  if (P > 1) {
-    st_g1r(&sh[tid], acc);
-    __syncthreads();
-    for (uint32_t h = P >> 1; h >= 1; h >>= 1) {
-      if (s < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
-      __syncthreads();
-    }
-    if (s == 0 && b < B) bsum[(size_t)slot * B + b] = sh[tid];
-  } else if (b < B) {
-    st_g1r(&bsum[(size_t)slot * B + b], acc);
+  for (uint32_t h = P >> 1; h >= 1; h >>= 1) {  // lanes s < h add lane s + h (same bucket)
+    G1R o;
+    o.X = shfl_down_rfp(acc.X, h);
+    o.Y = shfl_down_rfp(acc.Y, h);
+    o.ZZ = shfl_down_rfp(acc.ZZ, h);
+    o.ZZZ = shfl_down_rfp(acc.ZZZ, h);
+    if (s < h) acc = g1r_add(acc, o);
   }
+  if (s == 0 && b < B) st_g1r(&bsum[(size_t)slot * B + b], acc);
 }
 
 #ifndef PLK_RUNSUM_WAVES

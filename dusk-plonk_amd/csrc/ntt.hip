@@ -49,10 +49,13 @@ __device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
 using RFr = Rx<FrCfg>;
 constexpr int kL = RxShape<FrCfg>::L;
 
-// The data planes use a compile-time stride (the largest E): each limb access is then one
+// The data planes use a compile-time stride DS >= E: each limb access is then one
 // ds_read/ds_write with an immediate offset from a single address, instead of a v_add per
-// plane for a run-time stride.
+// plane for a run-time stride. Two strides: the largest E, and kDSSmall for passes of
+// E <= 256 (transforms up to 2^16), whose workgroups then hold 15 KiB of LDS instead of 38
+// (several proofs in flight share the CUs' LDS with the MSM's tree kernels).
 constexpr uint32_t kDS = 1u << kMaxLe;
+constexpr uint32_t kDSSmall = 256;
 
 // Element idx of a data plane sits at word idx ^ ((idx / 32) * 9 mod 32): ds_read_b32 /
 // ds_write_b32 bank by word mod 32 per 32-lane half, and the unswizzled columns put the
@@ -62,18 +65,20 @@ constexpr uint32_t kDS = 1u << kMaxLe;
 // kernel's index patterns, sizes 2^12 .. 2^23). A permutation of the low 5 bits: stays in [0, E).
 __device__ __forceinline__ uint32_t swz(uint32_t idx) { return idx ^ (((idx >> 5) * 9u) & 31u); }
 
+template <uint32_t DS>
 __device__ __forceinline__ RFr lds_ldd(const uint32_t* base, uint32_t idx) {
   RFr r;
   idx = swz(idx);
 #pragma unroll
-  for (int l = 0; l < kL; ++l) r.v[l] = base[l * kDS + idx];
+  for (int l = 0; l < kL; ++l) r.v[l] = base[l * DS + idx];
   return r;
 }
 
+template <uint32_t DS>
 __device__ __forceinline__ void lds_std(uint32_t* base, uint32_t idx, const RFr& v) {
   idx = swz(idx);
 #pragma unroll
-  for (int l = 0; l < kL; ++l) base[l * kDS + idx] = v.v[l];
+  for (int l = 0; l < kL; ++l) base[l * DS + idx] = v.v[l];
 }
 
 __device__ __forceinline__ RFr lds_ld(const uint32_t* base, uint32_t stride, uint32_t idx) {
@@ -188,7 +193,7 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
 // with x_(j+R/8) = 0 except for j = 0 — the 8n coset transforms of the prover's
 // (n + small)-coefficient polynomials. They are computed directly from the loaded rows
 // (7 multiplies per row instead of three stages of butterflies over 8x the rows).
-template <int PRE, int POST, int PRUNE>
+template <int PRE, int POST, int PRUNE, uint32_t DS>
 __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                   const Fr* __restrict__ tw,
                                                   const Fr* __restrict__ ptw,
@@ -201,8 +206,8 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   const uint32_t E = R << lt, H = R >> 1;
   // kL planes of the TS inner twiddles w_R^x (x < R/2; x < R when pruning)
   const uint32_t TS = PRUNE ? R : H;
-  uint32_t* data = smem32;          // kL planes of E (stride kDS)
-  uint32_t* twl = smem32 + kL * kDS;
+  uint32_t* data = smem32;          // kL planes of E (stride DS >= E)
+  uint32_t* twl = smem32 + kL * DS;
   uint32_t* ztab = twl + kL * TS;   // kZTab (reduce_q)
 
   // vector blockIdx.y of a batch: its input, output and scale-table rows
@@ -242,7 +247,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
         const uint32_t blk = 4 * hs + q, b = bitrev(blk, 3);
         RFr v = (j == 0 || b == 0) ? x : rx_mul(x, lds_ld(twl, TS, j * b));
         if (has8) v = rx_add(v, b == 0 ? x8 : rx_mul(x8, lds_ld(twl, TS, R8 * b)));
-        lds_std(data, ((blk * R8 + j) << lt) + t, v);
+        lds_std<DS>(data, ((blk * R8 + j) << lt) + t, v);
       }
     }
   }
@@ -285,7 +290,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
         if (PRE == 1) v = rx_mul(v, rx_unpack(aux[c]));
       }
       if (PRE != 1 && lp != 0 && j != 0 && (i & (p - 1)) != 0) v = rx_mul(v, rx_unpack(aux[c]));
-      if (e < E) lds_std(data, (j << lt) + t, v);
+      if (e < E) lds_std<DS>(data, (j << lt) + t, v);
     }
   }
   __syncthreads();
@@ -304,8 +309,8 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       const uint32_t j = ((jg >> (lh - 1)) << (lh + 1)) + r;
       const uint32_t i0 = (j << lt) + t, i1 = ((j + h) << lt) + t;
       const uint32_t i2 = ((j + 2 * h) << lt) + t, i3 = ((j + 3 * h) << lt) + t;
-      const RFr x0 = lds_ldd(data, i0), x1 = lds_ldd(data, i1);
-      const RFr x2 = lds_ldd(data, i2), x3 = lds_ldd(data, i3);
+      const RFr x0 = lds_ldd<DS>(data, i0), x1 = lds_ldd<DS>(data, i1);
+      const RFr x2 = lds_ldd<DS>(data, i2), x3 = lds_ldd<DS>(data, i3);
       // inputs: normalised, < 5r. Stage of half 2h: twiddle w^(r s1) for x0/x2 (identity
       // when r = 0), w^((r+h) s1) for x1/x3; sums y0, y1 unnormalised (limbs < 2^30, < 10r)
       const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
@@ -313,15 +318,15 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
                             : reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 2r / < 4r
       const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, (r + h) << sh1));
       // stage of half h: twiddle w^(r s2) for both pairs; outputs normalised, < 5r
-      lds_std(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
-      lds_std(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 6r -> < 4r
+      lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
+      lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 6r -> < 4r
       if (r != 0) {
         const RFr w = lds_ld(twl, TS, r << sh2);
-        lds_std(data, i1, rx_mul(sub_u2<11>(y0, y1), w));         // (y0 - y1 + 11r) w
-        lds_std(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 4r
+        lds_std<DS>(data, i1, rx_mul(sub_u2<11>(y0, y1), w));         // (y0 - y1 + 11r) w
+        lds_std<DS>(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 4r
       } else {
-        lds_std(data, i1, reduce_q(sub_u2<11>(y0, y1), ztab));     // < 21r -> < 4r
-        lds_std(data, i3, reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab));
+        lds_std<DS>(data, i1, reduce_q(sub_u2<11>(y0, y1), ztab));     // < 21r -> < 4r
+        lds_std<DS>(data, i3, reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab));
       }
     }
     __syncthreads();
@@ -330,10 +335,10 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
     for (uint32_t b = tid; b < (E >> 1); b += bd) {
       const uint32_t t = b & (T - 1), jb = b >> lt;
       const uint32_t j1 = jb << 1;
-      const RFr a = lds_ldd(data, (j1 << lt) + t);
-      const RFr c = lds_ldd(data, ((j1 + 1) << lt) + t);
-      lds_std(data, (j1 << lt) + t, reduce_q(add_u(a, c), ztab));
-      lds_std(data, ((j1 + 1) << lt) + t, reduce_q(rx_sub_u<FrCfg, 6>(a, c), ztab));
+      const RFr a = lds_ldd<DS>(data, (j1 << lt) + t);
+      const RFr c = lds_ldd<DS>(data, ((j1 + 1) << lt) + t);
+      lds_std<DS>(data, (j1 << lt) + t, reduce_q(add_u(a, c), ztab));
+      lds_std<DS>(data, ((j1 + 1) << lt) + t, reduce_q(rx_sub_u<FrCfg, 6>(a, c), ztab));
     }
     __syncthreads();
   }
@@ -351,7 +356,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
     const uint32_t i = i0 + t;
     const uint32_t k = i & (p - 1);
     const size_t pos = ((size_t)(i - k) << lr) + k + ((size_t)m << lp);
-    RFr v = lds_ldd(data, (bitrev(m, lr) << lt) + t);  // < 5r
+    RFr v = lds_ldd<DS>(data, (bitrev(m, lr) << lt) + t);  // < 5r
     if (POST == 1) v = rx_mul(v, rx_unpack(post_scalar));
     else if (POST == 2) v = rx_mul(v, ld_rfr(&post[pos]));
     else v = reduce_q(v, ztab);  // < 1.6r
@@ -546,7 +551,9 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     // zero-padded input (rows j <= R/8 of the first pass only): closed-form first stages
     const bool prune = first && !last && ps.lr >= 4 &&
                        len_in <= ((n >> ps.lr) << (ps.lr - 3)) + (n >> ps.lr);
-    const size_t lds = ((size_t)kDS + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) * kL * sizeof(uint32_t);
+    const bool small = E <= kDSSmall;
+    const size_t lds = ((size_t)(small ? kDSSmall : kDS) + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
+                       kL * sizeof(uint32_t);
     dim3 grid(blocks, count);
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
@@ -555,11 +562,16 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     str.out = last ? bt.out_stride : n * 1;
     str.pre = bt.pre ? bt.pre_stride : 0;
     str.post = bt.post ? bt.post_stride : 0;
-#define PLK_LAUNCH(PRE, POST, PRUNE)                                                    \
-  hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE>), grid, dim3(bd), lds, stream, src, dst, tw, ptw, \
-                     pre_table ? pre_table : d->coset_pow.as<Fr>(),                    \
+#define PLK_LAUNCH_DS(PRE, POST, PRUNE, DS)                                               \
+  hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE, DS>), grid, dim3(bd), lds, stream, src, dst, tw, \
+                     ptw, pre_table ? pre_table : d->coset_pow.as<Fr>(),               \
                      bt.post ? bt.post : d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n, \
                      ps.lp, ps.lr, ps.lt, lin, str)
+#define PLK_LAUNCH(PRE, POST, PRUNE)                    \
+  do {                                                  \
+    if (small) PLK_LAUNCH_DS(PRE, POST, PRUNE, kDSSmall); \
+    else PLK_LAUNCH_DS(PRE, POST, PRUNE, kDS);          \
+  } while (0)
     if (prune) {
       if (pre == 1) PLK_LAUNCH(1, 0, 1);
       else PLK_LAUNCH(0, 0, 1);
@@ -569,6 +581,7 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     else if (pre == 0 && post == 2) PLK_LAUNCH(0, 2, 0);
     else if (pre == 1 && post == 1) PLK_LAUNCH(1, 1, 0);
     else PLK_LAUNCH(1, 2, 0);
+#undef PLK_LAUNCH_DS
 #undef PLK_LAUNCH
     PLK_HIP_TRY(hipGetLastError());
     src = dst;
