@@ -61,9 +61,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=0,
                     help="concurrent prover lanes per GPU (prove mode): independent contexts "
                          "with their own streams, each driven by a host thread. 0 = 8 at "
-                         "n >= 2^18, 12 below (tools/gpu_queues.sh with 2 HIP hardware queues "
-                         "per lane: 2^20 23.5/24.1/24.4/24.2 M and 2^16 14.9/17.0/17.3/18.6 M "
-                         "constraints/s at 3/6/8/12 lanes)")
+                         "n >= 2^18, 12 at 2^15..2^17, 16 below (2 HIP hardware queues per "
+                         "lane; tools/gpu_lanes_small.sh: 2^16 20.7/21.0/22.0/21.1 M and "
+                         "2^12 3.25/3.60/3.78/3.82 M constraints/s at 10/12/14/16 lanes)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4); "
                          "0 = min(32, 2 x lanes): more lanes than queues serialise on them")
@@ -714,8 +714,8 @@ def main():
         raise SystemExit(launch_ranks(args.gpus))
     if world_env is not None and args.gpus is not None and args.gpus != int(world_env):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
-    if args.lanes <= 0:
-        args.lanes = 8 if args.log_n >= 18 else 12
+    if args.lanes <= 0:  # tools/gpu_lanes_small.sh: 2^12 3.6 -> 3.9 M at 12 -> 16 lanes
+        args.lanes = 8 if args.log_n >= 18 else 12 if args.log_n >= 15 else 16
     if args.mode == "prove":
         # before the HIP runtime starts (the torch import below): each lane's stream gets a
         # hardware queue of its own
