@@ -314,19 +314,27 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       // inputs: normalised, < 5r. Stage of half 2h: twiddle w^(r s1) for x0/x2 (identity
       // when r = 0), w^((r+h) s1) for x1/x3; sums y0, y1 unnormalised (limbs < 2^30, < 10r)
       const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
-      const RFr y2 = r != 0 ? rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), lds_ld(twl, TS, r << sh1))
-                            : reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 2r / < 4r
-      const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, (r + h) << sh1));
-      // stage of half h: twiddle w^(r s2) for both pairs; outputs normalised, < 5r
-      lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
-      lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 6r -> < 4r
-      if (r != 0) {
-        const RFr w = lds_ld(twl, TS, r << sh2);
-        lds_std<DS>(data, i1, rx_mul(sub_u2<11>(y0, y1), w));         // (y0 - y1 + 11r) w
-        lds_std<DS>(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 4r
-      } else {
-        lds_std<DS>(data, i1, reduce_q(sub_u2<11>(y0, y1), ztab));     // < 21r -> < 4r
+      if (h == 1) {  // r = 0 in every group: no twiddle on x0 / x2 nor in the second stage
+        const RFr y2 = reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 4r
+        const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, 1u << sh1));
+        lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));            // < 20r -> < 4r
+        lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));            // < 6r -> < 4r
+        lds_std<DS>(data, i1, reduce_q(sub_u2<11>(y0, y1), ztab));       // < 21r -> < 4r
         lds_std<DS>(data, i3, reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab));
+      } else {
+        // r = 0 groups multiply by w^0 = 1 (twl[0]) under the same bounds as r != 0: the
+        // lanes of a wave mix both (columns T < 64), so a branch ran both paths, and
+        // straight-line code leaves three independent products (y2, y3, output 1) to
+        // interleave. Stage of half h: twiddle w^(r s2) for both pairs; outputs normalised
+        const RFr w1 = lds_ld(twl, TS, r << sh1), w2 = lds_ld(twl, TS, (r + h) << sh1);
+        const RFr w = lds_ld(twl, TS, r << sh2);
+        const RFr y2 = rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), w1);  // < 2r
+        const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), w2);
+        const RFr o1 = rx_mul(sub_u2<11>(y0, y1), w);          // (y0 - y1 + 11r) w
+        lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
+        lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 4r
+        lds_std<DS>(data, i1, o1);
+        lds_std<DS>(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 2r
       }
     }
     __syncthreads();
