@@ -148,6 +148,23 @@ def test_device_entry_points(plk, gpu_ctx, oracle):
     assert np.array_equal(out.cpu().numpy().view(np.uint64), x)
 
 
+@pytest.mark.parametrize("k", [5, 12, 20])
+def test_device_null_input(plk, gpu_ctx, k):
+    """plk_ntt_dev with len_in = 0 and no input buffer (a zero polynomial): every transform
+    writes n zeros. The pass kernel's loads are unconditional, so the host points them at a
+    live table (ntt.hip `no_input`); single- and multi-pass plans."""
+    import torch
+    n = 1 << k
+    f = plk.Fft(k, gpu_ctx)
+    out = torch.full((n, 4), -1, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for direction, coset in ((1, False), (1, True), (-1, False), (-1, True)):
+        out.fill_(-1)
+        f.ntt_dev(0, out.data_ptr(), 0, direction, coset, stream)
+        torch.cuda.synchronize()
+        assert not out.cpu().numpy().any(), (k, direction, coset)
+
+
 @pytest.mark.parametrize("k", [6, 12, 16, 20])
 def test_zero_padded_first_pass(plk, gpu_ctx, oracle, k):
     """Inputs of at most n/8 + n/R coefficients take the closed-form first stages of the
