@@ -57,6 +57,19 @@ constexpr int kL = RxShape<FrCfg>::L;
 constexpr uint32_t kDS = 1u << kMaxLe;
 constexpr uint32_t kDSSmall = 256;
 
+// -DPLK_NTT_FUSE=1: the first radix-4 step on the loaded registers (k_ntt_pass), one LDS
+// round trip fewer per pass. Parity-green, measured within noise (2^20 6.85 / 6.89, 2^23
+// 8.48 / 8.37 G points/s fused / not, tools/gpu_ntt_ab.sh) and 131 VGPRs (3 waves per SIMD
+// instead of the 4 the LDS allows; capped at 128 it spills and runs 3 % slower): off
+#ifndef PLK_NTT_FUSE
+#define PLK_NTT_FUSE 0
+#endif
+constexpr bool kFuseFirstStep = PLK_NTT_FUSE != 0;
+// k_ntt_pass minimum waves per SIMD (-DPLK_NTT_MINW=4 caps it at 128 VGPRs)
+#ifndef PLK_NTT_MINW
+#define PLK_NTT_MINW 1
+#endif
+
 // Element idx of a data plane sits at word idx ^ ((idx / 32) * 9 mod 32): ds_read_b32 /
 // ds_write_b32 bank by word mod 32 per 32-lane half, and the unswizzled columns put the
 // bit-reversed output reads on one bank (32-way at the first pass of 2^20 / 2^23: ~15 us of a
@@ -182,6 +195,41 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
   return r;
 }
 
+// Two radix-2 DIF stages (halves 2h and h) on rows x0..x3 = j, j+h, j+2h, j+3h of one
+// column (r = j mod h), stored back to LDS at i0..i3. Inputs normalised, < 5r.
+template <uint32_t DS>
+__device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uint32_t TS,
+                                        const uint32_t* ztab, uint32_t r, uint32_t h,
+                                        uint32_t sh1, uint32_t sh2, uint32_t i0, uint32_t i1,
+                                        uint32_t i2, uint32_t i3, const RFr& x0, const RFr& x1,
+                                        const RFr& x2, const RFr& x3) {
+  // inputs: normalised, < 5r. Stage of half 2h: twiddle w^(r s1) for x0/x2 (identity
+  // when r = 0), w^((r+h) s1) for x1/x3; sums y0, y1 unnormalised (limbs < 2^30, < 10r)
+  const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
+  if (h == 1) {  // r = 0 in every group: no twiddle on x0 / x2 nor in the second stage
+    const RFr y2 = reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 4r
+    const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, 1u << sh1));
+    lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));            // < 20r -> < 4r
+    lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));            // < 6r -> < 4r
+    lds_std<DS>(data, i1, reduce_q(sub_u2<11>(y0, y1), ztab));       // < 21r -> < 4r
+    lds_std<DS>(data, i3, reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab));
+  } else {
+    // r = 0 groups multiply by w^0 = 1 (twl[0]) under the same bounds as r != 0: the
+    // lanes of a wave mix both (columns T < 64), so a branch ran both paths, and
+    // straight-line code leaves three independent products (y2, y3, output 1) to
+    // interleave. Stage of half h: twiddle w^(r s2) for both pairs; outputs normalised
+    const RFr w1 = lds_ld(twl, TS, r << sh1), w2 = lds_ld(twl, TS, (r + h) << sh1);
+    const RFr w = lds_ld(twl, TS, r << sh2);
+    const RFr y2 = rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), w1);  // < 2r
+    const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), w2);
+    const RFr o1 = rx_mul(sub_u2<11>(y0, y1), w);          // (y0 - y1 + 11r) w
+    lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
+    lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 4r
+    lds_std<DS>(data, i1, o1);
+    lds_std<DS>(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 2r
+  }
+}
+
 // One Stockham pass. PRE: 0 none, 1 multiply input e by pre[e] (coset g^e).
 // POST: 0 none, 1 multiply by post_scalar, 2 multiply output e by post[e].
 // Data buffers are R-domain (canonical in and out); tw / pre / post / post_scalar are
@@ -194,7 +242,7 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
 // (n + small)-coefficient polynomials. They are computed directly from the loaded rows
 // (7 multiplies per row instead of three stages of butterflies over 8x the rows).
 template <int PRE, int POST, int PRUNE, uint32_t DS>
-__global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
+__global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                   const Fr* __restrict__ tw,
                                                   const Fr* __restrict__ ptw,
                                                   const Fr* __restrict__ pre,
@@ -223,6 +271,12 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   for (uint32_t x = tid; x < TS; x += bd) lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
   for (uint32_t x = tid; x < kQMax * kL; x += bd) ztab[x] = kZTab.v[x];
 
+  // radix-2 stages left: the first radix-4 step's half is 2^(lh-1) (three stages done in
+  // closed form when pruning)
+  int lh = (int)lr - 1 - (PRUNE ? 3 : 0);
+  // first radix-4 step fused into the load phase (uniform): a thread's four elements form
+  // one of its groups when E = 4 bd
+  const bool fuse = kFuseFirstStep && !PRUNE && lr >= 2 && E == 4 * bd;
   if (PRUNE) {
     __syncthreads();
     // item = (row j < R/8, column t, half hs): blocks 4 hs .. 4 hs + 3 of (j, t)
@@ -277,9 +331,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
         aux[c] = ld_fr(&ptw[((size_t)(e >> lt) << lp) + ((i0 + (e & (T - 1))) & (p - 1))]);
       }
     }
-#pragma unroll
-    for (uint32_t c = 0; c < kLoadIt; ++c) {
-      if (c >= nit) break;
+    auto input = [&](uint32_t c) -> RFr {  // element tid + c bd, pre-scaled / twiddled
       const uint32_t e = tid + c * bd;
       const uint32_t t = e & (T - 1), j = e >> lt;
       const uint32_t i = i0 + t;
@@ -290,7 +342,26 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
         if (PRE == 1) v = rx_mul(v, rx_unpack(aux[c]));
       }
       if (PRE != 1 && lp != 0 && j != 0 && (i & (p - 1)) != 0) v = rx_mul(v, rx_unpack(aux[c]));
-      if (e < E) lds_std<DS>(data, (j << lt) + t, v);
+      return v;
+    };
+    if (fuse) {
+      // E = 4 bd: the thread's elements are rows j, j + R/4, j + R/2, j + 3R/4 of column t
+      // (j = tid >> lt < R/4) — exactly one group of the first radix-4 step (halves R/2 and
+      // R/4), which therefore runs on the loaded registers: one LDS round trip fewer
+      __syncthreads();  // twl / ztab staged
+      const uint32_t t = tid & (T - 1), j = tid >> lt, h = R >> 2;
+      const RFr x0 = input(0), x1 = input(1), x2 = input(2), x3 = input(3);
+      r4_step<DS>(data, twl, TS, ztab, j, h, 0, 1, (j << lt) + t, ((j + h) << lt) + t,
+                  ((j + 2 * h) << lt) + t, ((j + 3 * h) << lt) + t, x0, x1, x2, x3);
+      lh -= 2;
+    } else {
+#pragma unroll
+      for (uint32_t c = 0; c < kLoadIt; ++c) {
+        if (c >= nit) break;
+        const uint32_t e = tid + c * bd;
+        const RFr v = input(c);
+        if (e < E) lds_std<DS>(data, ((e >> lt) << lt) + (e & (T - 1)), v);
+      }
     }
   }
   __syncthreads();
@@ -299,7 +370,6 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
   // per LDS round trip: a thread loads x0..x3 = rows j, j+h, j+2h, j+3h, applies the stage
   // of half 2h (pairs x0/x2, x1/x3) and the stage of half h (pairs y0/y1, y2/y3) in
   // registers, and stores once. Same butterflies and twiddles as stage-by-stage radix 2.
-  int lh = (int)lr - 1 - (PRUNE ? 3 : 0);
   for (; lh >= 1; lh -= 2) {
     const uint32_t h = 1u << (lh - 1);
     const uint32_t sh1 = lr - 1 - lh, sh2 = lr - lh;  // twiddle index shifts of both stages
@@ -311,31 +381,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(const Fr* __restrict__ in, Fr*
       const uint32_t i2 = ((j + 2 * h) << lt) + t, i3 = ((j + 3 * h) << lt) + t;
       const RFr x0 = lds_ldd<DS>(data, i0), x1 = lds_ldd<DS>(data, i1);
       const RFr x2 = lds_ldd<DS>(data, i2), x3 = lds_ldd<DS>(data, i3);
-      // inputs: normalised, < 5r. Stage of half 2h: twiddle w^(r s1) for x0/x2 (identity
-      // when r = 0), w^((r+h) s1) for x1/x3; sums y0, y1 unnormalised (limbs < 2^30, < 10r)
-      const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
-      if (h == 1) {  // r = 0 in every group: no twiddle on x0 / x2 nor in the second stage
-        const RFr y2 = reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 4r
-        const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, 1u << sh1));
-        lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));            // < 20r -> < 4r
-        lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));            // < 6r -> < 4r
-        lds_std<DS>(data, i1, reduce_q(sub_u2<11>(y0, y1), ztab));       // < 21r -> < 4r
-        lds_std<DS>(data, i3, reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab));
-      } else {
-        // r = 0 groups multiply by w^0 = 1 (twl[0]) under the same bounds as r != 0: the
-        // lanes of a wave mix both (columns T < 64), so a branch ran both paths, and
-        // straight-line code leaves three independent products (y2, y3, output 1) to
-        // interleave. Stage of half h: twiddle w^(r s2) for both pairs; outputs normalised
-        const RFr w1 = lds_ld(twl, TS, r << sh1), w2 = lds_ld(twl, TS, (r + h) << sh1);
-        const RFr w = lds_ld(twl, TS, r << sh2);
-        const RFr y2 = rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), w1);  // < 2r
-        const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), w2);
-        const RFr o1 = rx_mul(sub_u2<11>(y0, y1), w);          // (y0 - y1 + 11r) w
-        lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
-        lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 4r
-        lds_std<DS>(data, i1, o1);
-        lds_std<DS>(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 2r
-      }
+      r4_step<DS>(data, twl, TS, ztab, r, h, sh1, sh2, i0, i1, i2, i3, x0, x1, x2, x3);
     }
     __syncthreads();
   }
