@@ -721,7 +721,7 @@ __global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, u
 // bit i of a set; A_g is the sum of the rows: 480 + 71 additions per 256 buckets instead of
 // the 1 144 of bit sums taken over the buckets themselves.
 // k_bitsum1 (one workgroup of 256 lanes per g): the bucket sums S (k_bucket_sum), the 32
-// row / column sums (8 lanes each: one addition, then a 3-level LDS tree),
+// row / column sums (8 consecutive lanes each: one addition, then a 3-level shuffle tree),
 // then the 9 outputs from them (wave 0). out[slot][g][0..7] = T_j(g), [8] = A_g; with `zin`
 // (wide bucket sets) also [9] = the plain sum of the group's 256 Z values (k_runsum).
 constexpr uint32_t kBitsumOut = 10;
@@ -735,62 +735,63 @@ template <bool Z>
 __global__ void __launch_bounds__(Z ? 384 : 256) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
                                                            const G1xyzz* __restrict__ zin,
                                                            G1xyzz* __restrict__ out) {
-  // [0, NV): the group's values (buckets or run sums Y; with Z also the 256 plain-sum values),
-  // [NV, NV + NS): row / column sums (and the 16 row sums of the plain-sum values)
-  constexpr uint32_t NV = Z ? 512 : 256, NS = Z ? 48 : 32;
-  __shared__ G1xyzz sh[NV + NS];
+  // the group's values (buckets or run sums Y; with Z also the 256 plain-sum values) are
+  // read straight from HBM and the trees run over cross-lane shuffles: LDS holds only the
+  // NS row / column sums (9 KiB instead of 105 — a resident k_bitsum1 used to keep the other
+  // proofs' NTT passes off its CU)
+  constexpr uint32_t NS = Z ? 48 : 32;
+  __shared__ G1xyzz sh[NS];
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
   out += ((size_t)slot * gridDim.x + g) * kBitsumOut;
-  for (uint32_t x = tid; x < NV; x += blockDim.x) {
+  auto value = [&](uint32_t x) -> G1R {  // x < 256: bsum, else zin; past B: infinity
     const uint32_t b = g * 256 + (x & 255);
     const G1xyzz* src = x < 256 ? bsum : zin;
-    if (b < B) sh[x] = src[(size_t)slot * B + b];
-    else st_g1r(&sh[x], g1r_infinity());
-  }
-  __syncthreads();
+    return b < B ? ld_g1r(&src[(size_t)slot * B + b]) : g1r_infinity();
+  };
+  auto shfl_down_g1r = [](const G1R& v, uint32_t h) {
+    G1R o;
+    o.X = shfl_down_rfp(v.X, h);
+    o.Y = shfl_down_rfp(v.Y, h);
+    o.ZZ = shfl_down_rfp(v.ZZ, h);
+    o.ZZZ = shfl_down_rfp(v.ZZZ, h);
+    return o;
+  };
   {  // sum q < 16: row a = q; 16 <= q < 32: column c = q - 16; q >= 32 (Z): row q - 32 of the
-     // plain-sum values. Lane e of its 8 adds members 2e, 2e + 1.
+     // plain-sum values. Lane e of its 8 (consecutive lanes) adds members 2e, 2e + 1.
     const uint32_t q = tid >> 3, e = tid & 7;
     const uint32_t m0 = q < 16 ? 16 * q + 2 * e : q < 32 ? (q - 16) + 32 * e : 256 + 16 * (q - 32) + 2 * e;
     const uint32_t m1 = (q >= 16 && q < 32) ? m0 + 16 : m0 + 1;
-    const G1R acc = g1r_add(ld_g1r(&sh[m0]), ld_g1r(&sh[m1]));
-    __syncthreads();
-    st_g1r(&sh[tid], acc);
-    __syncthreads();
+    G1R acc = g1r_add(value(m0), value(m1));
     for (uint32_t h = 4; h >= 1; h >>= 1) {
-      if (e < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
-      __syncthreads();
+      const G1R o = shfl_down_g1r(acc, h);
+      if (e < h) acc = g1r_add(acc, o);
     }
-    if (e == 0) sh[NV + q] = sh[tid];
+    if (e == 0) st_g1r(&sh[q], acc);
     __syncthreads();
   }
   // wave 0: lanes 0..31 = T_0..T_7, 4 lanes each (2 terms per lane); lanes 32..39 = A_g, 8 lanes
   // (rows 2e, 2e + 1); with Z lanes 40..47 = the plain sum (its rows 2e, 2e + 1); then trees
-  if (tid < (Z ? 48u : 40u)) {
+  if (tid < 64) {
+    const bool on = tid < (Z ? 48u : 40u);
     const uint32_t s = tid < 32 ? tid >> 2 : tid < 40 ? 8 : 9, e = tid < 32 ? tid & 3 : (tid - 32) & 7;
     const uint32_t w = tid < 32 ? 4 : 8;
-    uint32_t i0, i1;
+    uint32_t i0 = 0, i1 = 0;
     if (s < 4) {  // columns c with bit s
-      i0 = NV + 16 + with_bit(2 * e, s);
-      i1 = NV + 16 + with_bit(2 * e + 1, s);
+      i0 = 16 + with_bit(2 * e, s);
+      i1 = 16 + with_bit(2 * e + 1, s);
     } else if (s < 8) {  // rows a with bit s - 4
-      i0 = NV + with_bit(2 * e, s - 4);
-      i1 = NV + with_bit(2 * e + 1, s - 4);
-    } else {  // all rows (A_g) / all plain-sum rows
-      i0 = NV + (s == 8 ? 0 : 32) + 2 * e;
+      i0 = with_bit(2 * e, s - 4);
+      i1 = with_bit(2 * e + 1, s - 4);
+    } else if (on) {  // all rows (A_g) / all plain-sum rows
+      i0 = (s == 8 ? 0 : 32) + 2 * e;
       i1 = i0 + 1;
     }
-    st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[i0]), ld_g1r(&sh[i1])));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (uint32_t h = 4; h >= 1; h >>= 1) {
-      if (e < h && h < w) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    G1R acc = on ? g1r_add(ld_g1r(&sh[i0]), ld_g1r(&sh[i1])) : g1r_infinity();
+    for (uint32_t h = 4; h >= 1; h >>= 1) {  // groups of w consecutive lanes
+      const G1R o = shfl_down_g1r(acc, h);
+      if (on && e < h && h < w) acc = g1r_add(acc, o);
     }
-    if (e == 0) out[s] = sh[tid];
+    if (on && e == 0) st_g1r(&out[s], acc);
   }
 }
 
