@@ -801,7 +801,7 @@ __global__ void __launch_bounds__(Z ? 384 : 256) k_bitsum1(uint32_t B, const G1x
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, uint32_t nout,
                                                  G1xyzz* __restrict__ out) {
-  __shared__ G1xyzz sh[256];
+  __shared__ G1xyzz sh[4];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
   in += (size_t)slot * G * kBitsumOut;
   G1R acc = g1r_infinity();
@@ -816,13 +816,23 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
       acc = g1r_add(acc, ld_g1r(&e[8]));
     }
   }
-  st_g1r(&sh[tid], acc);
-  __syncthreads();
-  for (uint32_t h = min(G, 256u) >> 1; h >= 1; h >>= 1) {  // lanes >= G hold infinity
-    if (tid < h) st_g1r(&sh[tid], g1r_add(ld_g1r(&sh[tid]), ld_g1r(&sh[tid + h])));
-    __syncthreads();
+  // lanes >= G hold infinity: a shuffle tree over each wave's min(G, 64) lanes, then the
+  // wave totals through LDS (768 B instead of a 48 KiB tree)
+  for (uint32_t h = min(G, 64u) >> 1; h >= 1; h >>= 1) {
+    G1R o;
+    o.X = shfl_down_rfp(acc.X, h);
+    o.Y = shfl_down_rfp(acc.Y, h);
+    o.ZZ = shfl_down_rfp(acc.ZZ, h);
+    o.ZZZ = shfl_down_rfp(acc.ZZZ, h);
+    if ((tid & 63) < h) acc = g1r_add(acc, o);
   }
-  if (tid == 0) out[(size_t)slot * nout + j] = sh[0];
+  const uint32_t nw = min(G, 256u) > 64 ? min(G, 256u) >> 6 : 1;  // waves holding values
+  if ((tid & 63) == 0 && (tid >> 6) < nw) st_g1r(&sh[tid >> 6], acc);
+  __syncthreads();
+  if (tid == 0) {
+    for (uint32_t w = 1; w < nw; ++w) acc = g1r_add(acc, ld_g1r(&sh[w]));
+    st_g1r(&out[(size_t)slot * nout + j], acc);
+  }
 }
 
 // flag[slot] |= any nonzero scalar in [len, check_len)  (commit degree check)
