@@ -36,13 +36,39 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-# The accumulation's own ceiling: v_mad_u64_u32 issue rate (tools/ubench_mad.hip: 3.53e13/s
-# chip-wide at 4 waves/SIMD, 3.2e13 at 2; dependent latency = issue cost) over the mads of
-# one XYZZ mixed addition in the redundant Fp form (ffr.hpp / g1r.hpp): 8 products x 196 +
-# 2 squares x 105 + 9 Montgomery reductions x 196 (Y3 = R(Q - X3) - Y1 PPP is one fused
-# sum of two products) = 3542, the count of v_mad_u64_u32 in the compiled loop body.
+# The accumulation's own ceiling: v_mad_u64_u32 issue rate. The guide lists no integer-mad
+# peak; this one is MEASURED by tools/ubench_mad.hip (3.53e13/s chip-wide at 4 waves/SIMD,
+# 3.2e13 at 2; dependent latency = issue cost).
 VALU_MAD_PEAK = 3.53e13
+FR_MUL_PEAK = 1.64e11  # ffr.hpp Fr multiplies/s chip-wide, tools/ubench_limbs.hip (measured)
+VALU_MAD_PEAK_SOURCE = ("measured by tools/ubench_mad.hip (independent v_mad_u64_u32 chains, "
+                        "4 waves/SIMD, whole chip); MI355X_MICROARCH.md lists no integer-mad peak")
+# Formula count of one XYZZ mixed addition in the redundant Fp form (ffr.hpp / g1r.hpp):
+# 8 products x 196 + 2 squares x 105 + 9 Montgomery reductions x 196; used only when the
+# compiled count (tools/isa_count.py on libplk.so) cannot be read.
 MADS_PER_MIXED_ADD = 8 * 196 + 2 * 105 + 9 * 196
+_ISA = {}
+
+
+def compiled_loop(kernel: str = "k_accumulateILb0E") -> dict:
+    """v_mad_u64_u32 / instructions of the kernel's loop body as compiled (largest basic
+    block of its gfx950 code in libplk.so, tools/isa_count.py)."""
+    if kernel not in _ISA:
+        try:
+            sys.path.insert(0, str(ROOT / "tools"))
+            import isa_count
+            lib = os.environ.get("PLK_LIB") or str(ROOT / "dusk-plonk_amd" / "libplk.so")
+            r = isa_count.largest_block(Path(lib), kernel)
+            _ISA[kernel] = ({"v_mad_u64_u32": r["v_mad_u64_u32"], "instructions": r["instructions"],
+                             "source": "compiled loop body (tools/isa_count.py on libplk.so)"}
+                            if r else None)
+        except Exception as e:  # noqa: BLE001 — llvm-objdump missing: formula fallback
+            _ISA[kernel] = {"v_mad_u64_u32": MADS_PER_MIXED_ADD, "instructions": None,
+                            "source": f"formula (compiled count unavailable: {e!r})"}
+        if _ISA[kernel] is None:
+            _ISA[kernel] = {"v_mad_u64_u32": MADS_PER_MIXED_ADD, "instructions": None,
+                            "source": "formula (kernel not found in libplk.so)"}
+    return _ISA[kernel]
 
 
 def parse():
@@ -364,11 +390,31 @@ def host_info():
 
 
 def valu_roofline(adds_per_s):
-    """k_accumulate against its binding ceiling: v_mad_u64_u32 issue (mads/s)."""
-    achieved = adds_per_s * MADS_PER_MIXED_ADD
-    return {"bound": "valu (v_mad_u64_u32 issue)", "achieved": achieved, "peak": VALU_MAD_PEAK,
-            "unit": "mad/s", "frac": achieved / VALU_MAD_PEAK,
-            "mads_per_point_add": MADS_PER_MIXED_ADD}
+    """k_accumulate against its binding ceiling: v_mad_u64_u32 issue (mads/s), with the mads
+    per mixed addition counted in the compiled loop."""
+    isa = compiled_loop()
+    achieved = adds_per_s * isa["v_mad_u64_u32"]
+    return {"bound": "valu", "achieved": achieved, "peak": VALU_MAD_PEAK, "unit": "mad/s",
+            "frac": achieved / VALU_MAD_PEAK, "peak_source": VALU_MAD_PEAK_SOURCE,
+            "mads_per_point_add": isa["v_mad_u64_u32"],
+            "instructions_per_point_add": isa["instructions"], "mads_source": isa["source"]}
+
+
+def binding_roofline(valu: dict, hbm_achieved_gbs: float, alg_bytes: float, traffic,
+                     kernel: str) -> dict:
+    """The roofline object of the bench line: the BINDING (integer-VALU) roofline at top level
+    (bound / achieved / peak / frac), HBM as the required secondary figure under `hbm`, and
+    `traffic` = PMC-measured HBM bytes per launch."""
+    return {"bound": "valu", "kernel": kernel, "achieved": valu["achieved"], "peak": valu["peak"],
+            "unit": "mad/s", "frac": valu["frac"], "peak_source": valu["peak_source"],
+            "mads_per_point_add": valu["mads_per_point_add"],
+            "instructions_per_point_add": valu["instructions_per_point_add"],
+            "mads_source": valu["mads_source"], "traffic": traffic,
+            "hbm": {"achieved": hbm_achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm_achieved_gbs / HBM_PEAK_GBS,
+                    "algorithmic_bytes_per_launch": alg_bytes,
+                    "note": "secondary roofline: SURVEY §8d algorithmic bytes (128 B per MSM point)"
+                            " over the average launch"}}
 
 
 def load_pmc_traffic(kernel_substr: str, key: str = "hbm_bytes_per_launch",
@@ -436,15 +482,18 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
     # sharded: every rank proves the same proofs (same seeds), commits split by SRS slice
     lane_seed = (lambda l: 17 + 101 * l) if shard else (lambda l: 1000 * rank + 17 + 101 * l)
     lanes = [ProofLane(base, lane_seed(l)) for l in range(L)]
+    exchange = None
     if shard:
-        from dusk_plonk_amd.parallel import shard_prover_lane, srs_slice
+        from dusk_plonk_amd.parallel import ExchangeService, shard_prover_lane, srs_slice
         comm_dev = device if dist.get_backend() == "nccl" else None
         sl = srs_slice(base.tau, base.pp.n, world, rank, ctx)  # one slice per GPU, all lanes
-        # one process group per lane: a lane's exchanges are ordered within its own group,
-        # lanes run concurrently (every rank creates the groups in the same order)
-        groups = [dist.new_group(backend=dist.get_backend()) for _ in range(L)]
-        for ln, g in zip(lanes, groups):
-            shard_prover_lane(ln.lane, base.tau, base.pp.n, g, comm_dev, ctx, slice_=sl)
+        # every lane's exchanges on ONE communicator, issued by ONE thread per rank in the
+        # order rank 0 sequences (parallel.ExchangeService: no concurrent collectives on
+        # different communicators, so no cross-rank ordering deadlock)
+        exchange = ExchangeService(None, comm_dev)
+        for l, ln in enumerate(lanes):
+            shard_prover_lane(ln.lane, base.tau, base.pp.n, None, comm_dev, ctx, slice_=sl,
+                              exchange=exchange, lane_id=l)
     import concurrent.futures as cf
     drivers = cf.ThreadPoolExecutor(L)
 
@@ -531,10 +580,10 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
                if launches and acc_ms > 0 else None)
         traffic = load_pmc_traffic("k_accumulate")
         traffic2 = load_pmc_traffic("k_accumulate", "hbm_bytes_per_launch_stream_corrected")
-        result["roofline"] = {
-            "bound": "hbm", "kernel": "k_accumulate", "achieved": solo["achieved_gbs"],
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": solo["achieved_gbs"] / HBM_PEAK_GBS,
-            "traffic": traffic, "traffic_fetch_doubled": traffic2,
+        roof = binding_roofline(solo["valu"], solo["achieved_gbs"],
+                                solo["algorithmic_bytes_per_launch"], traffic, "k_accumulate")
+        roof.update({
+            "traffic_fetch_doubled": traffic2,
             "traffic_source": ("stored profile profiles/pmc_traffic.json (rocprofv3 --pmc "
                                "FETCH_SIZE / WRITE_SIZE passes of the default bench command, "
                                "per-launch average over the run); `traffic` = raw FETCH + WRITE, "
@@ -542,16 +591,15 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
                                "16-B/lane streams — this kernel's 96-B random gathers are an "
                                "uncalibrated width, so the two bracket it")
             if traffic is not None else None,
-            "algorithmic_bytes_per_launch": solo["algorithmic_bytes_per_launch"],
             "avg_launch_ms": solo["avg_launch_ms"], "launches": solo["launches"],
             "point_adds_per_launch": solo["point_adds_per_launch"],
             "point_adds_per_s": solo["point_adds_per_s"],
-            "valu": solo["valu"], "binding_roofline": "valu",
             "solo": solo, "in_workload": inw,
-            "note": "integer-VALU-bound (no MFMA): the binding fraction is valu.frac "
-                    "(v_mad_u64_u32 issue); HBM reported as the required secondary roofline "
-                    "(4 commit batches per proof: 4, 1, 4 and 2 MSMs)",
-        }
+            "note": "integer-VALU-bound (no MFMA): frac = v_mad_u64_u32 issue of the solo "
+                    "launches against the measured mad peak; HBM under `hbm` (4 commit batches "
+                    "per proof: 4, 1, 4 and 2 MSMs)",
+        })
+        result["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_full(k, base.pp, cpu_threads(args))
     if rank == 0:
@@ -559,6 +607,8 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
     for ln in lanes:
         ln.pool.shutdown(wait=True)
         ln.lane.close()
+    if exchange is not None:
+        exchange.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -627,6 +677,12 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
                 "unit": "GB/s", "traffic": load_pmc_traffic("k_ntt_pass", fname=f"pmc_traffic_ntt{k}.json"),
                 "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": launch_ms,
                 "dft_ms": t_dft, "idft_ms": t_idft,
+                # the radix-2 butterflies' Fr multiplications against the measured redundant-
+                # limb Fr multiply rate (tools/ubench_limbs.hip): the instruction-side floor
+                "valu": {"achieved": (n / 2) * k / (launch_ms * 1e-3), "peak": FR_MUL_PEAK,
+                         "unit": "Fr mul/s", "frac": (n / 2) * k / (launch_ms * 1e-3) / FR_MUL_PEAK,
+                         "peak_source": "measured by tools/ubench_limbs.hip (ffr.hpp Fr multiply, "
+                                        "whole chip)", "ops": "(N/2) log2 N butterflies"},
                 "note": "per transform (all its Stockham passes; traffic summed over them); "
                         "instruction-bound, see DESIGN §3"}
         metric = f"standalone BlsScalar dft+idft points/s at n=2^{k} (BASELINE configs[1])"
@@ -635,16 +691,17 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
         launch_ms = sum(e[0] for e in ev) / steps
         adds = sum(e[1] for e in ev) / steps
         alg_bytes = 128.0 * n  # N * (32 B scalar + 96 B base)
-        roof = {"bound": "hbm", "kernel": "k_accumulate", "achieved":
-                alg_bytes / (launch_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "traffic": load_pmc_traffic("k_accumulate", fname=f"pmc_traffic_msm{k}.json"),
-                "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": launch_ms,
-                "point_adds_per_launch": adds, "point_adds_per_s": adds / (launch_ms * 1e-3),
-                "valu": valu_roofline(adds / (launch_ms * 1e-3)),
-                "note": "integer-VALU-bound (no MFMA); HBM is the secondary roofline"}
+        gbs = alg_bytes / (launch_ms * 1e-3) / 1e9
+        roof = binding_roofline(valu_roofline(adds / (launch_ms * 1e-3)), gbs, alg_bytes,
+                                load_pmc_traffic("k_accumulate", fname=f"pmc_traffic_msm{k}.json"),
+                                "k_accumulate")
+        roof.update({"avg_launch_ms": launch_ms, "point_adds_per_launch": adds,
+                     "point_adds_per_s": adds / (launch_ms * 1e-3),
+                     "note": "integer-VALU-bound (no MFMA); HBM is the secondary roofline"})
         metric = f"standalone G1 MSM points/s at n=2^{k} (BASELINE configs[2])"
         workload = f"KZG10 commit: one 2^{k}-point G1 MSM, random Fr scalars, SRS bases"
-    roof["frac"] = roof["achieved"] / roof["peak"]
+    if "frac" not in roof:
+        roof["frac"] = roof["achieved"] / roof["peak"]
     result = {
         "metric": metric, "value": units * steps * world / elapsed, "unit": "points/s",
         "n_gpus": world, "steps": steps, "warmup": args.warmup,

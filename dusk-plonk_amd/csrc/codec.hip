@@ -10,7 +10,9 @@
 // is [u64; 4] Montgomery limbs, little-endian = 32 bytes; ProofEvaluations in the order the
 // prover builds it (linearization_poly.rs:117-134), the order of plk_proof. SCALE's Decode
 // of a bool rejects bytes other than 0 and 1; this decoder also rejects limbs that are not
-// canonical and points off y^2 = x^3 + 4 (the curve check the verifier relies on).
+// canonical and finite points off y^2 = x^3 + 4 (the curve check the verifier relies on).
+// The identity is encoded (x = 0, y = 0, is_infinity = 1); on decode any canonical
+// coordinates under the flag mean the identity (zkcrypto crates write y = one).
 // Host code only.
 #include <cstring>
 
@@ -113,8 +115,11 @@ int plk_proof_decode(const uint8_t* in, size_t len, plk_proof* proof) {
     g->infinity = q[96];
     if (!canonical<FpCfg>(g->x) || !canonical<FpCfg>(g->y)) return PLK_E_ARG;
     if (g->infinity) {
-      for (int k = 0; k < 6; ++k)
-        if (g->x[k] | g->y[k]) return PLK_E_ARG;  // the identity is (0, 0, true)
+      // the flag alone marks the identity: zkcrypto-style crates write (0, one, true), this
+      // encoder (0, 0, true); a derived Decode keeps whatever coordinates came, so any
+      // canonical pair is accepted and normalised to this ABI's (0, 0, 1)
+      std::memset(g->x, 0, sizeof g->x);
+      std::memset(g->y, 0, sizeof g->y);
     } else if (!on_curve(*g)) {
       return PLK_E_ARG;
     }

@@ -863,7 +863,10 @@ static G1xyzz rx_to_r_domain(const G1xyzz& p) {
 }
 
 int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
-  if (len <= w.cap_len && slots <= w.cap_slots && w.cap_len) return PLK_OK;
+  const bool same_shape = w.cap_c == s->c && w.cap_windows == s->windows;
+  if (same_shape && len <= w.cap_len && slots <= w.cap_slots && w.cap_len) return PLK_OK;
+  // buffers only ever grow (DevBuf::alloc), so re-sizing for another shape keeps the larger
+  // of the old and new needs; the strides below always match the current shape
   len = std::max(len, w.cap_len);
   slots = std::max(slots, w.cap_slots);
   const size_t B = (size_t)1 << (s->c - 1);
@@ -909,6 +912,8 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   w.cap_len = len;
   w.cap_slots = slots;
+  w.cap_c = s->c;
+  w.cap_windows = s->windows;
   w.task_stride = max_tasks;
   w.sorted_stride = entries + 1;
   return PLK_OK;

@@ -81,6 +81,10 @@ struct MsmWorkspace {
   PinnedBuf host_out;  // per-slot bit sums T, flags and entry counts read back by the host
   size_t cap_len = 0, task_stride = 0, sorted_stride = 0;
   uint32_t cap_slots = 0;
+  // the SRS shape the buffers and strides were sized for: a workspace moves between SRSs
+  // (a prover's key SRS, then a shard slice with another window size), and every size
+  // above depends on c and the window count
+  uint32_t cap_c = 0, cap_windows = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   MsmStats stats;
   ~MsmWorkspace() {

@@ -324,9 +324,10 @@ int key_commit(plk_key* key, MsmWorkspace& ws, const std::vector<const Fr*>& ptr
 // The same commit group split over the ranks of a sharded prover (plk_prover_shard, SURVEY
 // §8e): this rank's MSMs over its SRS slice [lo, hi) of every polynomial, one all-gather
 // of (13 point words + status) per commit, and the fold of the partial points in rank order.
-// The last rank also checks the tail [max_points, len) for the degree error. Every rank
-// takes part in the exchange even when its own MSMs failed, so no rank waits forever on a
-// collective the others left.
+// The last rank also checks the tail [max_points, len) for the degree error, wherever that
+// tail starts relative to its slice (an SRS longer than the circuit's trimmed one puts the
+// last slice past it). Every rank takes part in the exchange even when its own MSMs failed,
+// so no rank waits forever on a collective the others left.
 int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
                  const std::vector<size_t>& lens, plk_g1* outs, int* statuses, size_t cap) {
   plk_key* key = P->key;
@@ -342,11 +343,17 @@ int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
     const size_t use = std::min(lens[i], max_points);
     luse[i] = use > lo ? (size_t)(std::min<uint64_t>(use, hi) - lo) : 0;
     lchk[i] = luse[i];
-    if (last && lens[i] > use) {
-      if (use < lo) local = PLK_E_ARG;  // the tail would start before this slice
-      else lchk[i] = lens[i] - lo;
-    }
     lp[i] = ptrs[i] + lo;
+    if (last && lens[i] > use) {
+      if (use >= lo) {
+        lchk[i] = lens[i] - lo;  // the tail follows this slice's own points
+      } else {
+        // nothing of this polynomial falls in the slice: an empty MSM whose base is the
+        // start of the tail, so the degree check reads [use, lens) (no SRS point is read)
+        lp[i] = ptrs[i] + use;
+        lchk[i] = lens[i] - use;
+      }
+    }
   }
   std::vector<plk_g1> part(cnt, plk_g1{});
   std::vector<int> pst(cnt, PLK_OK);
@@ -969,23 +976,21 @@ int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int ra
 int plk_prove(plk_key* key, const plk_composer* cs, uint64_t seed, plk_proof* proof,
               plk_fr* public_inputs, size_t pi_cap, size_t* pi_count) {
   if (!key) return PLK_E_ARG;
-  plk_prover* p;
-  {
-    std::lock_guard<std::mutex> lk(key->def_mu);
-    if (!key->def_prover) {
-      try {
-        std::unique_ptr<plk_prover> d(new plk_prover());
-        d->key = key;
-        d->ws = msm_workspace_new();
-        d->stream = key->ctx->stream;  // the context's stream, not owned
-        key->def_prover = std::move(d);
-      } catch (const std::bad_alloc&) {
-        return PLK_E_OOM;
-      }
+  // the default prover's scratch, workspace and stream serve one proof at a time: concurrent
+  // plk_prove calls on one key run one after the other (plk_prover_create gives parallel lanes)
+  std::lock_guard<std::mutex> lk(key->def_mu);
+  if (!key->def_prover) {
+    try {
+      std::unique_ptr<plk_prover> d(new plk_prover());
+      d->key = key;
+      d->ws = msm_workspace_new();
+      d->stream = key->ctx->stream;  // the context's stream, not owned
+      key->def_prover = std::move(d);
+    } catch (const std::bad_alloc&) {
+      return PLK_E_OOM;
     }
-    p = key->def_prover.get();
   }
-  return plk_prover_prove(p, cs, seed, proof, public_inputs, pi_cap, pi_count);
+  return plk_prover_prove(key->def_prover.get(), cs, seed, proof, public_inputs, pi_cap, pi_count);
 }
 
 int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_proof* proof,

@@ -14,9 +14,15 @@ The full prover uses the same split inside ``plk_prover_prove`` (BASELINE config
 as the C ABI's ``plk_allgather_fn``; every rank then proves the same circuit with the same
 seed, runs the NTT / elementwise rounds as replicas and splits each of the proof's 4 commit
 groups (wires, z, quotient chunks, openings: prover.rs:133-136,194,262-265,440,452) by SRS
-index — one all-gather of 14 words per commit per group, host fold on every rank.
+index — one all-gather of 14 words per commit per group, host fold on every rank. With
+several lanes per rank, ``ExchangeService`` runs every lane's all-gathers on one
+communicator from one thread, in an order rank 0 sequences (deadlock-free by construction).
 """
 from __future__ import annotations
+
+import threading
+import time
+from collections import deque
 
 import numpy as np
 
@@ -71,6 +77,189 @@ def torch_allgather(group=None, device=None):
     return allgather
 
 
+class _Request:
+    __slots__ = ("data", "done", "result", "error")
+
+    def __init__(self, data: bytes):
+        self.data = data
+        self.done = threading.Event()
+        self.result = None
+        self.error = None
+
+
+class ExchangeService:
+    """The all-gathers of every prover lane of this rank on ONE communicator, issued by ONE
+    thread, in an order every rank agrees on — deadlock-free by construction.
+
+    With one communicator per lane, lanes reach their exchanges in timing-dependent order, so
+    ranks could launch RCCL collectives on different communicators in different orders while
+    other lanes' kernels hold the CUs — the pattern that can deadlock. Here:
+      * every lane's `allgather` only queues its request and waits for the result;
+      * rank 0's exchange thread picks the lanes whose requests are pending on rank 0 (arrival
+        order) and broadcasts that list (lane id + byte count per entry) to every rank;
+      * every rank's exchange thread then waits until those lanes' requests are pending
+        locally and runs ONE all-gather of their payloads concatenated in list order.
+    Collectives are thus issued by one thread per rank on one group, in the same sequence on
+    every rank. A rank only ever waits for a lane's NEXT request, and the lanes' request
+    sequences are identical on every rank (every rank proves the same proofs with the same
+    seeds; a commit's status travels in the exchange, so every rank takes the same error
+    path), so each awaited request arrives: lanes never wait on anything but their own
+    exchange. `close()` (every rank, after its lanes stopped) ends the thread: rank 0
+    broadcasts a stop entry once nothing is pending.
+    """
+
+    MAX_BATCH = 64  # lanes served by one all-gather
+    REQUEST_TIMEOUT_S = 600.0  # a lane rank 0 scheduled must reach its exchange by then
+
+    def __init__(self, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.group, self.device = group, device
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.src = dist.get_global_rank(group, 0) if group is not None else 0
+        self.cv = threading.Condition()
+        self.pending = {}        # lane -> deque of _Request (a lane has at most one)
+        self.arrivals = deque()  # rank 0: lane ids in arrival order
+        self.closing = False
+        self.error = None
+        self.exchanges = 0       # all-gathers run (statistics)
+        self.requests = 0        # lane requests served
+        self.thread = threading.Thread(target=self._run, name="plk-exchange", daemon=True)
+        self.thread.start()
+
+    def allgather_for(self, lane: int):
+        """`allgather(send: bytes) -> bytes` for prover lane `lane` (the same id on every
+        rank): every rank's bytes concatenated in rank order."""
+        def allgather(data: bytes) -> bytes:
+            req = _Request(bytes(data))
+            with self.cv:
+                if self.error is not None:
+                    raise RuntimeError(f"exchange service failed: {self.error!r}")
+                if self.closing:
+                    raise RuntimeError("exchange service closed")
+                self.pending.setdefault(lane, deque()).append(req)
+                self.arrivals.append(lane)
+                self.cv.notify_all()
+            req.done.wait()
+            if req.error is not None:
+                raise RuntimeError(f"exchange failed: {req.error!r}")
+            return req.result
+        return allgather
+
+    # -- exchange thread -----------------------------------------------------------------
+    def _tensor(self, arr):
+        t = self.torch.from_numpy(arr)
+        return t.to(self.device) if self.device is not None else t
+
+    def _plan(self):
+        """Rank 0: (lanes, sizes) to serve next, or None to stop."""
+        with self.cv:
+            while not self.arrivals and not (self.closing and not self._any_pending()):
+                self.cv.wait()
+            if not self.arrivals:
+                return None
+            lanes, seen = [], set()
+            while self.arrivals and len(lanes) < self.MAX_BATCH:
+                ln = self.arrivals[0]
+                if ln in seen:  # a lane's next request waits for the next all-gather
+                    break
+                self.arrivals.popleft()
+                seen.add(ln)
+                lanes.append(ln)
+            return lanes, [len(self.pending[ln][0].data) for ln in lanes]
+
+    def _any_pending(self):
+        return any(self.pending.values())
+
+    def _run(self):
+        torch, dist = self.torch, self.dist
+        header = np.zeros(1 + 2 * self.MAX_BATCH, dtype=np.int64)
+        stream = torch.cuda.Stream(device=self.device) if self.device is not None else None
+        try:
+            while True:
+                if self.rank == 0:
+                    plan = self._plan()
+                    header[:] = 0
+                    if plan is None:
+                        header[0] = -1
+                    else:
+                        lanes, sizes = plan
+                        header[0] = len(lanes)
+                        header[1:1 + len(lanes)] = lanes
+                        header[1 + self.MAX_BATCH:1 + self.MAX_BATCH + len(lanes)] = sizes
+                with (torch.cuda.stream(stream) if stream is not None else _nullctx()):
+                    h = self._tensor(header.copy())
+                    dist.broadcast(h, src=self.src, group=self.group)
+                    hdr = h.cpu().numpy()
+                    cnt = int(hdr[0])
+                    if cnt < 0:
+                        return
+                    lanes = [int(x) for x in hdr[1:1 + cnt]]
+                    sizes = [int(x) for x in hdr[1 + self.MAX_BATCH:1 + self.MAX_BATCH + cnt]]
+                    reqs = []
+                    with self.cv:
+                        for ln in lanes:
+                            deadline = time.monotonic() + self.REQUEST_TIMEOUT_S
+                            while not self.pending.get(ln):
+                                left = deadline - time.monotonic()
+                                if left <= 0:  # the ranks' lane sequences diverged
+                                    raise RuntimeError(f"lane {ln}'s exchange never arrived "
+                                                       f"on rank {self.rank}")
+                                self.cv.wait(left)
+                            reqs.append(self.pending[ln].popleft())
+                        if self.rank != 0:  # keep the arrival log bounded off rank 0
+                            self.arrivals.clear()
+                    for r, sz in zip(reqs, sizes):
+                        if len(r.data) != sz:
+                            raise RuntimeError(f"lane exchange size differs across ranks "
+                                               f"({len(r.data)} here, {sz} on rank 0)")
+                    payload = b"".join(r.data for r in reqs)
+                    total = len(payload)
+                    t = self._tensor(np.frombuffer(payload, dtype=np.uint8).copy())
+                    out = torch.empty(self.world * total, dtype=torch.uint8, device=t.device)
+                    dist.all_gather_into_tensor(out, t, group=self.group)
+                    allb = out.cpu().numpy().tobytes()
+                self.exchanges += 1
+                self.requests += len(reqs)
+                off = 0
+                for r, sz in zip(reqs, sizes):
+                    r.result = b"".join(allb[q * total + off: q * total + off + sz]
+                                        for q in range(self.world))
+                    off += sz
+                    r.done.set()
+        except BaseException as e:  # noqa: BLE001 — every waiting lane must wake
+            with self.cv:
+                self.error = e
+                for dq in self.pending.values():
+                    for r in dq:
+                        r.error = e
+                        r.done.set()
+                    dq.clear()
+                self.cv.notify_all()
+
+    def close(self, timeout: float | None = 120.0):
+        """Stop the exchange thread (call on every rank once its lanes are done)."""
+        with self.cv:
+            self.closing = True
+            self.cv.notify_all()
+        self.thread.join(timeout)
+        if self.thread.is_alive():
+            raise RuntimeError("exchange thread did not stop")
+        if self.error is not None:
+            raise RuntimeError(f"exchange service failed: {self.error!r}")
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def srs_slice(tau, n_points: int, world: int, rank: int, ctx=None):
     """(slice start, PlonkParams) of rank `rank`'s share of the first `n_points` SRS
     powers of `tau` (plk_srs_setup_range on its GPU, window table included)."""
@@ -79,16 +268,20 @@ def srs_slice(tau, n_points: int, world: int, rank: int, ctx=None):
 
 
 def shard_prover_lane(lane, tau, n_points: int, group=None, device=None, ctx=None,
-                      slice_=None):
+                      slice_=None, exchange: ExchangeService | None = None, lane_id: int = 0):
     """Split every commit of `lane` (a prover.ProverLane) over the ranks of `group`: this
-    rank's slice of the first `n_points` SRS powers of `tau` and the group's all-gather.
+    rank's slice of the first `n_points` SRS powers of `tau` and an all-gather.
     `slice_` = (start, PlonkParams) from srs_slice lets several lanes share one slice (the
-    SRS is read-only; each lane brings its own MSM workspace). Returns the slice."""
+    SRS is read-only; each lane brings its own MSM workspace). With several lanes per rank
+    pass `exchange` (one ExchangeService per rank) and a `lane_id` that names the same lane
+    on every rank: all lanes' exchanges then share one communicator and one issuing thread.
+    A lone lane may use the group's all-gather directly. Returns the slice."""
     import torch.distributed as dist
 
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     lo, sl = slice_ if slice_ is not None else srs_slice(tau, n_points, world, rank, ctx)
-    lane.shard(sl, lo, rank, world, torch_allgather(group, device))
+    ag = exchange.allgather_for(lane_id) if exchange is not None else torch_allgather(group, device)
+    lane.shard(sl, lo, rank, world, ag)
     return lo, sl
 
 
@@ -138,5 +331,5 @@ class ShardedPlonkParams:
         return r
 
 
-__all__ = ["ShardedPlonkParams", "gather_fold", "shard_range", "shard_prover_lane",
-           "srs_slice", "torch_allgather", "PLK_E_DEGREE"]
+__all__ = ["ExchangeService", "ShardedPlonkParams", "gather_fold", "shard_range",
+           "shard_prover_lane", "srs_slice", "torch_allgather", "PLK_E_DEGREE"]

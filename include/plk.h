@@ -243,7 +243,9 @@ int plk_prove(plk_key* key, const plk_composer* circuit, uint64_t seed, plk_proo
  * window table read-only (one copy per GPU however many proofs are in flight). Provers of
  * one key may run plk_prover_prove from different threads at the same time. Destroy every
  * prover of a key before the key. plk_prove(key, ...) is plk_prover_prove on a default
- * prover the key owns (on the context's stream). */
+ * prover the key owns (on the context's stream); it is thread-safe, but concurrent
+ * plk_prove calls on one key are serialised on that prover — use plk_prover_create for
+ * proofs in parallel. */
 typedef struct plk_prover plk_prover;
 int plk_prover_create(plk_key* key, plk_prover** out);
 int plk_prover_destroy(plk_prover* p);
@@ -283,7 +285,9 @@ int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int ra
  * fields x, y (Fq = [u64; 6] Montgomery limbs, LE) and is_infinity (bool, 1 byte) = 97 B;
  * Fr as [u64; 4] Montgomery limbs, LE = 32 B; ProofEvaluations in plk_proof order. Total
  * PLK_PROOF_SCALE_BYTES. Decode rejects (PLK_E_ARG) a wrong length, a non-boolean flag,
- * limbs >= the modulus, and points not on y^2 = x^3 + 4. */
+ * limbs >= the modulus, and finite points not on y^2 = x^3 + 4. The identity (ASSUMED
+ * encoding) is written as x = 0, y = 0, is_infinity = 1; decode takes is_infinity = 1 with
+ * any canonical x, y (e.g. zkcrypto's y = one) as the identity and returns it as (0, 0, 1). */
 #define PLK_PROOF_SCALE_BYTES (11 * 97 + 16 * 32)
 int plk_proof_encode(const plk_proof* proof, uint8_t* out, size_t cap, size_t* len);
 int plk_proof_decode(const uint8_t* in, size_t len, plk_proof* proof);

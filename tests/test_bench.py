@@ -72,6 +72,16 @@ def test_prove_mode_line():
     assert d["value"] == pytest.approx(4096 * 2 * 2 / (d["ms_per_step"] * 2e-3), rel=1e-6)
 
 
+def test_compiled_loop_mads():
+    """bench.py's mads per mixed addition come from the compiled k_accumulate loop in
+    libplk.so (tools/isa_count.py), not from the formula constant."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    isa = bench.compiled_loop()
+    assert "compiled" in isa["source"], isa
+    assert 3000 < isa["v_mad_u64_u32"] < isa["instructions"] < 6000
+
+
 def test_gpus_flag_must_match_launcher():
     """Under a launcher (WORLD_SIZE set) --gpus must agree with it: no silent n_gpus: 1."""
     env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
@@ -88,6 +98,9 @@ def test_prove_mode_line_has_solo_roofline():
     assert r["kernel"] == "k_accumulate" and r["solo"]["launches"] == 4  # one proof
     assert r["avg_launch_ms"] == r["solo"]["avg_launch_ms"]
     assert r["in_workload"]["launches"] == 2 * 2 * 4
+    # the binding roofline at top level, HBM as the secondary figure
+    assert r["bound"] == "valu" and r["unit"] == "mad/s" and r["hbm"]["unit"] == "GB/s"
+    assert r["mads_per_point_add"] > 3000 and "compiled" in r["mads_source"]
     assert "13 transforms" in d["config"]["workload"] and "1 public input" in d["config"]["workload"]
 
 

@@ -273,3 +273,204 @@ def _allgather_cb_worker(rank, world, port, q):
 def test_sharded_prover_exchange_gloo_world2():
     out = _spawn(_allgather_cb_worker, 2)
     assert out == {0: True, 1: True}
+
+
+def _exchange_service_worker(rank, world, port, q):
+    """parallel.ExchangeService (the sharded prover's exchange with several lanes per rank):
+    3 lanes per rank, each a thread doing its own sequence of all-gathers of varying size,
+    with lane timing skewed differently on every rank (so the lanes reach their exchanges in
+    a different order on each rank) and one lane driven through the same ctypes callback type
+    the C++ prover calls (plk_allgather_fn). Every result must be the rank-ordered
+    concatenation; the service must then stop cleanly. gloo, CPU only."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import ctypes as C
+    import random
+    import threading
+    import time
+    import torch.distributed as dist
+    from dusk_plonk_amd.parallel import ExchangeService
+    from dusk_plonk_amd.prover import ALLGATHER_FN
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        svc = ExchangeService()
+        L, counts = 3, [9, 7, 4]  # lanes stop after different numbers of exchanges
+
+        def payload(r, lane, j):
+            n = 14 * 8 * (1 + (lane + j) % 4)
+            return bytes(((r * 131 + lane * 17 + j * 7 + i) & 0xFF) for i in range(n))
+
+        errors = []
+
+        def lane_thread(lane):
+            ag = svc.allgather_for(lane)
+            rng = random.Random(1000 * rank + lane)
+            if lane == 1:  # through the C callback type, as prover.hip calls it
+                def cb(_u, send, nbytes, recv):
+                    data = ag(C.string_at(send, nbytes))
+                    C.memmove(recv, data, len(data))
+                    return 0
+                fn = ALLGATHER_FN(cb)
+
+                def call(data):
+                    src = C.create_string_buffer(data, len(data))
+                    dst = C.create_string_buffer(world * len(data))
+                    if fn(None, C.cast(src, C.c_void_p), len(data), C.cast(dst, C.c_void_p)) != 0:
+                        raise RuntimeError("callback failed")
+                    return dst.raw
+            else:
+                call = ag
+            for j in range(counts[lane]):
+                # skew: rank 0 runs lane 0 slow and lane 2 fast, rank 1 the reverse
+                slow = (lane == 0) if rank == 0 else (lane == 2)
+                time.sleep(rng.uniform(0.0, 0.03) + (0.02 if slow else 0.0))
+                got = call(payload(rank, lane, j))
+                want = b"".join(payload(r, lane, j) for r in range(world))
+                if got != want:
+                    errors.append((lane, j))
+        ts = [threading.Thread(target=lane_thread, args=(ln,)) for ln in range(L)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        ok = not errors and not any(t.is_alive() for t in ts)
+        svc.close()
+        ok &= svc.requests == sum(counts) and svc.exchanges <= sum(counts)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_service_skewed_lanes_gloo_world2():
+    out = _spawn(_exchange_service_worker, 2)
+    assert out == {0: True, 1: True}
+
+
+def _sharded_lanes_worker(rank, world, port, q, logn, lanes, srs_mult):
+    """configs[4]'s multi-lane form: `lanes` prover lanes per rank, each sharded over the
+    ranks through ONE parallel.ExchangeService, proving concurrently with rank-dependent
+    skew. The SRS holds srs_mult x (n + 8) points, so with srs_mult >= 4 the last rank's
+    slice starts past the trimmed SRS (the t_4 tail check must still run there), and the
+    full SRS and the slices take different MSM window sizes: lane 0 proves once unsharded
+    (full SRS, c = 17 wide buckets) before it is sharded (slices, c = 15), so its MSM
+    workspace changes shape. Every proof must equal the unsharded plk_prove's bytes; an
+    unsatisfied circuit fails with the degree error on every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import random
+    import threading
+    import time
+    import torch.distributed as dist
+    from oracle_lib import random_fr
+    import dusk_plonk_amd as plk
+    from dusk_plonk_amd.parallel import ExchangeService, shard_prover_lane, srs_slice
+    from dusk_plonk_amd.prover import Plonk, PlonkKey
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tau = random_fr(1, seed=93)[0]
+        ctx = plk.Context.default(0)
+        n = 1 << logn
+        pp = plk.PlonkParams.setup(logn, tau, ctx, n_points=srs_mult * (n + 8))
+
+        def circ(seed):
+            cs = Plonk()
+            cs.synthetic_chain(n - 15, seed)
+            cs.append_public(seed + 7)
+            return cs
+        prover, _ = PlonkKey.compile_composer(pp, b"lanes", circ(1))
+        seeds = list(range(3, 3 + 2 * lanes))
+        want = {s: prover.prove_composer(circ(s + 10), s)[0].raw_bytes() for s in seeds}
+        lns = [prover.lane() for _ in range(lanes)]
+        ok = lns[0].prove_composer(circ(seeds[0] + 10), seeds[0])[0].raw_bytes() == want[seeds[0]]
+        svc = ExchangeService()
+        sl = srs_slice(tau, pp.n, world, rank, ctx)
+        for i, ln in enumerate(lns):
+            shard_prover_lane(ln, tau, pp.n, slice_=sl, exchange=svc, lane_id=i)
+        results, errors = {}, []
+
+        def drive(i):
+            rng = random.Random(100 * rank + i)
+            try:
+                for s in seeds[i::lanes]:
+                    time.sleep(rng.uniform(0, 0.05) * (1 + (i + rank) % 2))
+                    results[s] = lns[i].prove_composer(circ(s + 10), s)[0].raw_bytes()
+                if i == lanes - 1:  # an unsatisfied circuit: the degree error everywhere
+                    bad = circ(20)
+                    bad.set_witness(5, 12345)
+                    try:
+                        lns[i].prove_composer(bad, 1)
+                        errors.append("bad circuit proved")
+                    except plk.PlonkError as e:
+                        if e.status != plk.PLK_E_DEGREE:
+                            errors.append(f"status {e.status}")
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+        ts = [threading.Thread(target=drive, args=(i,)) for i in range(lanes)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(600)
+        svc.close()
+        ok &= not errors and all(results.get(s) == want[s] for s in seeds)
+        for ln in lns:
+            ln.close()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_prover_lanes_exchange_service(plk, gpu_ctx):
+    """2 ranks x 3 lanes through one ExchangeService per rank; SRS 4x the circuit's."""
+    out = _spawn(_sharded_lanes_worker, 2, 14, 3, 4)
+    assert out == {0: True, 1: True}
+
+
+@pytest.mark.gpu
+def test_sharded_prover_three_ranks_large_srs(plk, gpu_ctx):
+    """3 ranks x 2 lanes, SRS 5x the circuit's: two ranks' slices lie past the trimmed SRS."""
+    out = _spawn(_sharded_lanes_worker, 3, 12, 2, 5)
+    assert out == {0: True, 1: True, 2: True}
+
+
+def _sharded_2_20_worker(rank, world, port, q):
+    """BASELINE configs[4] at its own size: the headline 2^20 bench circuit proved with every
+    commit split over the ranks (plk_prover_shard, gloo on one card here; RCCL over xGMI on a
+    node), byte for byte against the committed oracle fixture tests/golden/proof_2_20.npz."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(ROOT / "tests" / "golden")]
+    import torch.distributed as dist
+    import dusk_plonk_amd as plk
+    from dusk_plonk_amd.parallel import ExchangeService, shard_prover_lane
+    from dusk_plonk_amd.prover import PlonkKey
+    from make_proof_2_20 import BLIND_SEED, LABEL, LOG_N, TAU_SEED, circuit
+    from test_prover_oracle import tau_for
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = dict(np.load(ROOT / "tests" / "golden" / "proof_2_20.npz", allow_pickle=False))
+        tau, _ = tau_for(TAU_SEED)
+        ctx = plk.Context.default(0)
+        pp = plk.PlonkParams.setup(LOG_N, tau, ctx)
+        cs = circuit()
+        prover, vd = PlonkKey.compile_composer(pp, LABEL, cs)
+        ok = np.array_equal(vd.comms, g["vk"])
+        lane = prover.lane()
+        svc = ExchangeService()
+        shard_prover_lane(lane, tau, pp.n, ctx=ctx, exchange=svc, lane_id=0)
+        proof, _ = lane.prove_composer(cs, BLIND_SEED)
+        svc.close()
+        ok &= proof.to_bytes() == g["scale"].tobytes()
+        lane.close()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_prover_2_20_equals_fixture(plk, gpu_ctx):
+    out = _spawn(_sharded_2_20_worker, 2)
+    assert out == {0: True, 1: True}

@@ -57,8 +57,27 @@ def test_identity_commitment_round_trip(plk, fixture):
     assert Proof.from_bytes(data) == p
 
 
+FP = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+
+
+def test_identity_any_coordinates(plk, fixture):
+    """The flag alone marks the identity: zkcrypto-style (0, one, true) with one = 2^384 mod p
+    in Montgomery limbs decodes as the identity, normalised to (0, 0, 1)."""
+    from dusk_plonk_amd.prover import Proof
+    b = bytearray(fixture["scale"].tobytes())
+    off = 4 * 97  # z_comm
+    b[off: off + 48] = bytes(48)
+    b[off + 48: off + 96] = ((1 << 384) % FP).to_bytes(48, "little")
+    b[off + 96] = 1
+    q = Proof.from_bytes(bytes(b))
+    comms = fixture["comms"].copy()
+    comms[4] = 0
+    comms[4, 12] = 1
+    assert q == Proof.from_words(comms, fixture["evals"])
+
+
 @pytest.mark.parametrize("case", ["short", "long", "bool", "x_noncanonical", "off_curve",
-                                  "identity_nonzero", "eval_noncanonical"])
+                                  "identity_noncanonical", "eval_noncanonical"])
 def test_decode_rejects(plk, fixture, case):
     from dusk_plonk_amd.prover import Proof
     b = bytearray(fixture["scale"].tobytes())
@@ -72,8 +91,9 @@ def test_decode_rejects(plk, fixture, case):
         b[40:48] = (0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")  # top limb of a_comm.x >= p
     elif case == "off_curve":
         b[0] ^= 1
-    elif case == "identity_nonzero":
+    elif case == "identity_noncanonical":
         b[96] = 1
+        b[40:48] = (0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")
     elif case == "eval_noncanonical":
         off = 11 * 97
         b[off + 24: off + 32] = (0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")

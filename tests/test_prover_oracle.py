@@ -8,6 +8,8 @@ so the chain of evidence is: merlin's published vector pins both transcripts
 of proof.rs / verifier.rs / commitment_scheme.rs) and tampering is rejected; the GPU proof
 equals the oracle proof on the same circuit, SRS, label and blinding seed.
 """
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -316,3 +318,45 @@ def test_gpu_proof_equals_oracle_bench_2_16(plk, oracle):
     assert np.array_equal(raw[: 11 * 13].reshape(11, 13), ref["comms"])
     assert np.array_equal(raw[11 * 13:].reshape(16, 4), ref["evals"])
     assert len(pis) == 1 and pis == [fr_int(p) for p in ref["pis"]]
+
+
+GOLD_2_20 = Path(__file__).resolve().parent / "golden" / "proof_2_20.npz"
+
+
+def test_fixture_2_20_shape():
+    """The committed 2^20 headline fixture (tests/golden/make_proof_2_20.py: the restated CPU
+    prover on bench.py's circuit) is a complete proof: VK, 11 commitments, 16 evaluations,
+    one public input, and SCALE bytes that are the restated encoding of those words."""
+    import sys
+    sys.path.insert(0, str(GOLD_2_20.parent))
+    from make_proof_scale import scale_bytes
+    g = dict(np.load(GOLD_2_20, allow_pickle=False))
+    assert g["vk"].shape == (15, 13) and g["comms"].shape == (11, 13)
+    assert g["evals"].shape == (16, 4) and g["pis"].shape == (1, 4)
+    assert list(g["meta"]) == [20, 77, 7, 0x5EED]
+    assert scale_bytes(g["comms"], g["evals"]) == g["scale"].tobytes()
+    assert not any(int(c[12]) for c in g["comms"])  # no identity commitments
+
+
+@pytest.mark.gpu
+def test_gpu_proof_equals_oracle_fixture_2_20(plk):
+    """BASELINE's headline workload (n = 2^20, the bench circuit) pinned byte for byte: the
+    GPU proof equals the restated CPU prover's (committed fixture, /root/reference/src/
+    prover.rs:67-474 order) — verifier key, commitments, evaluations, public input and the
+    SCALE bytes of the Proof."""
+    import sys
+    sys.path.insert(0, str(GOLD_2_20.parent))
+    from make_proof_2_20 import BLIND_SEED, LABEL, LOG_N, TAU_SEED, circuit
+    from dusk_plonk_amd.prover import PlonkKey, fr_int
+    g = dict(np.load(GOLD_2_20, allow_pickle=False))
+    tau_limbs, _ = tau_for(TAU_SEED)
+    cs = circuit()
+    pp = plk.PlonkParams.setup(LOG_N, tau_limbs)
+    prover, vd = PlonkKey.compile_composer(pp, LABEL, cs)
+    assert np.array_equal(vd.comms, g["vk"]), "verifier key commitments differ"
+    proof, pis = prover.prove_composer(cs, BLIND_SEED)
+    raw = np.frombuffer(proof.raw_bytes(), dtype=np.uint64)
+    assert np.array_equal(raw[: 11 * 13].reshape(11, 13), g["comms"])
+    assert np.array_equal(raw[11 * 13:].reshape(16, 4), g["evals"])
+    assert pis == [fr_int(p) for p in g["pis"]]
+    assert proof.to_bytes() == g["scale"].tobytes()
