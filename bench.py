@@ -294,13 +294,70 @@ def cpu_baseline(k: int, pp, threads: int):
     }
 
 
-def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
+def cpu_share() -> dict:
+    """Cores this process may use: the affinity mask, capped by a cgroup CPU quota (the GPU
+    box gives each GPU a share of the machine), and the whole machine's count."""
+    hi = host_info()
+    usable = hi["usable_cores"] or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    avail = max(1, min(usable, int(quota))) if quota else usable
+    # the GPU box allots each GPU a CPU share and says so in OMP_NUM_THREADS: worker pools
+    # stay within it (the rest of the machine belongs to the other GPUs' jobs)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(env) if env.isdigit() and int(env) > 0 else None
+    if share:
+        avail = min(avail, share)
+    return {"available": avail, "affinity": usable, "cgroup_quota_cpus": quota,
+            "omp_num_threads": share, "machine_cores": hi["nproc"], "cpu_model": hi["cpu_model"]}
+
+
+def cpu_concurrent(gates, wit, srs, vk, procs: int, n: int) -> dict:
+    """MEASURED concurrent CPU proof throughput: `procs` independent restated-reference proofs
+    (tests/oracle_worker.py, one OS process and one thread each — the throughput-optimal way
+    to use cores for a prover whose quotient loop is sequential) started together.
+    rate_sum = sum of n / create_proof time over the processes (their proofs run at once);
+    window = procs * n / (last end - first create_proof start), which also charges any
+    non-overlap."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        f = Path(d) / "inputs.npz"
+        np.savez(f, gates=gates, witness=wit, srs=srs, vk=vk)
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        ps = [subprocess.Popen([sys.executable, str(ROOT / "tests" / "oracle_worker.py"), str(f),
+                                "1", str(100 + i)], stdout=subprocess.PIPE, text=True, env=env)
+              for i in range(procs)]
+        outs = []
+        for p in ps:
+            o, _ = p.communicate(timeout=900)
+            if p.returncode != 0:
+                raise RuntimeError(f"oracle worker failed ({p.returncode})")
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    rate_sum = sum(n / o["create_proof_s"] for o in outs)
+    window = max(o["end"] for o in outs) - min(o["prove_start"] for o in outs)
+    return {"value": rate_sum, "unit": "constraints/s", "procs": procs, "n": n,
+            "create_proof_s": [round(o["create_proof_s"], 3) for o in outs],
+            "window_value": procs * n / window, "window_s": window}
+
+
+def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=None):
     """Restated reference CPU prover (oracle/plk_prover_oracle.c: key compile + create_proof
     in the reference's order and cost structure, OpenMP where the reference uses rayon,
-    sequential where it is sequential — notably the quotient loop's one v_h inversion per
-    8n point, quotient_poly.rs:99-107). One full CPU proof at 2^k_sample is timed by
-    phase; its O(n) phases scale by n / 2^k_sample, and the MSM and NTT phases are timed
-    directly at the 2^k sizes (11 MSM(n), 11 NTT(n), 8 NTT(8n) per proof)."""
+    sequential where it is sequential — notably the quotient loop's one v_h inversion per 8n
+    point, quotient_poly.rs:99-107), two ways:
+      * value (MEASURED throughput): as many independent single-thread proofs at 2^k_sample as
+        this process has cores, run at once (cpu_concurrent) — the CPU used as a proof server
+        uses it. Per-constraint CPU cost grows with n (MSM window, NTT depth), so the 2^16
+        rate bounds the CPU's 2^20 throughput from above: the GPU/CPU ratio is conservative;
+      * latency: ONE proof on `threads` threads (the reference's rayon prover on the GPU's
+        CPU share): a full proof at 2^k_sample timed by phase, composed to 2^k with MSM / NTT
+        timed at the 2^k sizes; the direct 2^20 timing is profiles/r02_cpu_full_n20.json."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
     from dusk_plonk_amd.prover import Plonk
@@ -310,7 +367,8 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
     cs = bench_circuit(Plonk, ns - 15, 77)
     gates, wit = cs.export()
     trim = (1 << (gates.shape[0] + 6 - 1).bit_length()) + 8
-    res = orc.prove(gates, wit, pp.points(0, trim), b"cpu-baseline", 5, threads)
+    srs = pp.points(0, trim)
+    res = orc.prove(gates, wit, srs, b"cpu-baseline", 5, threads)
     tm = res["timing_ns"].astype(np.float64) / 1e9
     prove_s, msm_s, ntt_s = tm[6], tm[1], tm[2]
     other_s = prove_s - msm_s - ntt_s  # quotient loop, grand product, openings, transcript
@@ -332,44 +390,49 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16):
         orc.coset_dft(v8, k + 3, threads)
         t_ntt8 = time.perf_counter() - t0
         per_proof = 11 * t_msm + 11 * t_ntt + 8 * t_ntt8 + other_s * (n / ns)
-    # the same restated prover on ONE core, at 2^12 (seconds, not extrapolated)
-    k1 = min(k, 12)
-    cs1 = bench_circuit(Plonk, (1 << k1) - 15, 78)
-    g1, w1 = cs1.export()
-    trim1 = (1 << (g1.shape[0] + 6 - 1).bit_length()) + 8
-    r1 = orc.prove(g1, w1, pp.points(0, trim1), b"cpu-baseline-1", 5, 1)
-    one_core_s = float(r1["timing_ns"][6]) / 1e9  # create_proof phase (compile excluded)
-    hi = host_info()
-    return {
-        "value": n / per_proof, "unit": "constraints/s", "cores": threads, "kind": "port",
-        "host": hi,
-        "extrapolated": ks != k,
-        "measure": "latency of ONE proof on `cores` threads (the GPU value is the throughput of "
-                   "all its lanes' proofs in flight)",
-        "all_cores_projection": {
-            "cores": hi["usable_cores"],
-            "value": n / per_proof * (hi["usable_cores"] or threads) / threads,
-            "note": "upper bound: the measured rate scaled linearly to every core in the "
-                    "affinity mask (perfect scaling assumed; the GPU box allots "
-                    f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')} per GPU)"},
-        "node_throughput_upper_bound": {
-            "value": (hi["usable_cores"] or threads) * (1 << k1) / one_core_s,
-            "note": f"usable cores x the single-core rate at 2^{k1} (independent proofs, one per "
-                    "core; per-constraint cost grows with n, so this bounds the node's 2^"
-                    f"{k} throughput from above)"},
-        "single_core": {"n": 1 << k1, "seconds": one_core_s,
-                        "value": (1 << k1) / one_core_s, "unit": "constraints/s",
-                        "note": "full create_proof (key compile excluded) on 1 thread"},
-        "sample": (f"oracle/plk_prover_oracle.c (restated reference CPU prover, OpenMP {threads} "
-                   f"threads): one full create_proof at 2^{ks} = {prove_s:.2f} s "
-                   f"({ns / prove_s:.0f} constraints/s; MSM {msm_s:.2f} s, NTT {ntt_s:.2f} s, "
-                   f"quotient loop {tm[3]:.2f} s, grand product {tm[4]:.2f} s, openings "
-                   f"{tm[5]:.2f} s); " + (
-                       f"timed directly at 2^{k}: {per_proof:.2f} s per proof" if ks == k else
-                       f"per proof at 2^{k} = 11 x MSM(2^{k}) {t_msm:.2f} s + "
-                       f"11 x dft(2^{k}) {t_ntt:.3f} s + 8 x coset_dft(2^{k + 3}) {t_ntt8:.3f} s + "
-                       f"O(n) phases x {n // ns} = {per_proof:.1f} s")),
+    share = cpu_share()
+    conc = cpu_concurrent(gates, wit, srs, res["vk"], share["available"], ns)
+    direct = None
+    f = ROOT / "profiles" / "r02_cpu_full_n20.json"
+    if k == 20 and f.exists():
+        try:
+            direct = json.loads(f.read_text())
+        except ValueError:
+            direct = None
+    out = {
+        "value": conc["value"], "unit": "constraints/s", "cores": conc["procs"], "kind": "port",
+        "measure": (f"MEASURED throughput of {conc['procs']} concurrent independent proofs at "
+                    f"n=2^{ks} (one process and thread each, every core of this process's "
+                    "share); an upper bound of the CPU's 2^20 throughput"),
+        "host": share,
+        "concurrent": conc,
+        "latency": {
+            "value": n / per_proof, "unit": "constraints/s", "threads": threads, "n": n,
+            "seconds_per_proof": per_proof, "composed": ks != k,
+            "direct_2_20": ({"seconds": direct.get("create_proof_s", direct.get("seconds")),
+                             "source": "profiles/r02_cpu_full_n20.json"} if direct else None),
+            "note": "ONE proof on `threads` threads: the reference's own constraints/s reading"},
+        "sample": (f"oracle/plk_prover_oracle.c (restated reference CPU prover): "
+                   f"{conc['procs']} concurrent single-thread proofs at 2^{ks}, create_proof "
+                   f"{min(conc['create_proof_s']):.1f}-{max(conc['create_proof_s']):.1f} s each; "
+                   f"one 2^{ks} proof on {threads} threads = {prove_s:.2f} s (MSM {msm_s:.2f} s, "
+                   f"NTT {ntt_s:.2f} s, quotient loop {tm[3]:.2f} s, grand product {tm[4]:.2f} s, "
+                   f"openings {tm[5]:.2f} s)" + (
+                       "" if ks == k else
+                       f"; latency at 2^{k} = 11 x MSM(2^{k}) {t_msm:.2f} s + 11 x dft(2^{k}) "
+                       f"{t_ntt:.3f} s + 8 x coset_dft(2^{k + 3}) {t_ntt8:.3f} s + O(n) phases x "
+                       f"{n // ns} = {per_proof:.1f} s")),
     }
+    mc = share["machine_cores"] or conc["procs"]
+    out["node_projection"] = {
+        "value": conc["value"] * mc / conc["procs"], "cores": mc,
+        "note": f"the measured per-core throughput x all {mc} cores of the machine (independent "
+                "processes; not measured beyond this process's share)"}
+    if gpu_value:
+        out["ratio"] = {"gpu_over_cpu_share": gpu_value / conc["value"],
+                        "gpu_over_node_projection": gpu_value / out["node_projection"]["value"],
+                        "gpu_over_latency": gpu_value / out["latency"]["value"]}
+    return out
 
 
 def host_info():
@@ -601,7 +664,8 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
         })
         result["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_full(k, base.pp, cpu_threads(args))
+        result["cpu_baseline"] = cpu_baseline_full(k, base.pp, cpu_threads(args),
+                                                   gpu_value=result["value"])
     if rank == 0:
         print(json.dumps(result), flush=True)
     for ln in lanes:

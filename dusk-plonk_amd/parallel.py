@@ -99,7 +99,8 @@ class ExchangeService:
         order) and broadcasts that list (lane id + byte count per entry) to every rank;
       * every rank's exchange thread then waits until those lanes' requests are pending
         locally and runs ONE all-gather of their payloads concatenated in list order.
-    Collectives are thus issued by one thread per rank on one group, in the same sequence on
+    Collectives are thus issued by one thread per rank on one group — a group of the service's
+    own, so no other thread's collective can interleave with them — in the same sequence on
     every rank. A rank only ever waits for a lane's NEXT request, and the lanes' request
     sequences are identical on every rank (every rank proves the same proofs with the same
     seeds; a commit's status travels in the exchange, so every rank takes the same error
@@ -112,14 +113,20 @@ class ExchangeService:
     REQUEST_TIMEOUT_S = 600.0  # a lane rank 0 scheduled must reach its exchange by then
 
     def __init__(self, group=None, device=None):
+        """Collective: every rank of `group` (default: the world) constructs it at the same
+        point. The service runs on a process group of its own over the same ranks, so the
+        caller's collectives on `group` (barriers, timing reductions) never interleave with
+        the exchange thread's on another thread."""
         import torch
         import torch.distributed as dist
 
         self.torch, self.dist = torch, dist
-        self.group, self.device = group, device
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.src = dist.get_global_rank(group, 0) if group is not None else 0
+        ranks = dist.get_process_group_ranks(group) if group is not None else None
+        self.group = dist.new_group(ranks=ranks, backend=dist.get_backend(group))
+        self.device = device
+        self.world = dist.get_world_size(self.group)
+        self.rank = dist.get_rank(self.group)
+        self.src = dist.get_global_rank(self.group, 0)
         self.cv = threading.Condition()
         self.pending = {}        # lane -> deque of _Request (a lane has at most one)
         self.arrivals = deque()  # rank 0: lane ids in arrival order

@@ -332,6 +332,14 @@ def _exchange_service_worker(rank, world, port, q):
         ts = [threading.Thread(target=lane_thread, args=(ln,)) for ln in range(L)]
         for t in ts:
             t.start()
+        # the caller's own collectives on the default group run concurrently with the
+        # service's (bench.py's barriers / timing reductions): they must not interleave
+        import torch
+        for _ in range(5):
+            dist.barrier()
+            x = torch.ones(1)
+            dist.all_reduce(x)
+            time.sleep(0.01 * (1 + rank))
         for t in ts:
             t.join(120)
         ok = not errors and not any(t.is_alive() for t in ts)

@@ -49,3 +49,16 @@ busy += cur_e - cur_s
 n = sum(1 for r in many if int(r["Start_Timestamp"]) >= lo)
 print(f"multi-lane: last 60 % of the run {(T1 - lo) / 1e3:.0f} us, GPU busy (any kernel) "
       f"{100 * busy / (T1 - lo):.1f} %, {n} dispatches = {n / ((T1 - lo) / 1e9):.0f} /s")
+# average number of kernels executing at once over the busy time, and each kernel's share
+# of the summed kernel time in the multi-lane window
+tot = sum(e - s for s, e in iv)
+print(f"multi-lane: mean concurrency over busy time {tot / busy:.2f} kernels")
+kt = collections.defaultdict(float)
+kc = collections.Counter()
+for r in many:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    if e > lo:
+        kt[name(r)] += (e - max(s, lo))
+        kc[name(r)] += 1
+for k, v in sorted(kt.items(), key=lambda kv: -kv[1])[:16]:
+    print(f"  {k:44s} {kc[k]:6d} {100 * v / tot:5.1f} % of kernel time, avg {v / kc[k] / 1e3:7.1f} us")

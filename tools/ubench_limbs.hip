@@ -88,6 +88,79 @@ __device__ __forceinline__ void red_mul(uint32_t* r, const uint32_t* a, const ui
   r[L - 1] = (uint32_t)acc;
 }
 
+// Round 3 A/B: 13 x 30-bit Fp limbs, 169 + 169 mads per product instead
+// of 196 + 196. Columns no longer fit one 64-bit accumulator (up to 26 terms below 2^60), so
+// every column whose worst-case sum could reach 2^64 keeps the products and the reduction
+// terms in two accumulators and merges their low B bits and carries (bounds computed at
+// compile time from the limb bounds: inputs < 2^(32N) so the top limb has 32N - B(L-1) bits,
+// p's top limb fewer).
+template <class C, int L, int B>
+struct SplitPlan {
+  bool split[2 * L - 1];
+  constexpr SplitPlan() : split{} {
+    constexpr RedCfg<C, L, B> K = make_cfg<C, L, B>();
+    const int top_bits = 32 * C::N - B * (L - 1);
+    long double carry = 0;  // bound of the incoming carry
+    for (int k = 0; k < 2 * L - 1; ++k) {
+      long double sum = carry;
+      for (int i = 0; i < L; ++i) {
+        const int j = k - i;
+        if (j < 0 || j >= L) continue;
+        const long double ai = (i == L - 1) ? (long double)(1ull << top_bits) : (long double)(1ull << B);
+        const long double bj = (j == L - 1) ? (long double)(1ull << top_bits) : (long double)(1ull << B);
+        sum += ai * bj;                                    // a_i b_j
+        sum += (long double)(1ull << B) * (long double)(K.p[j] + 1);  // m_i p_j
+      }
+      split[k] = sum >= 18446744073709551616.0L;
+      carry = sum / (long double)(1ull << B) + 2;
+    }
+  }
+};
+
+template <class C, int L, int B>
+__device__ __forceinline__ void red_mul_split(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  constexpr RedCfg<C, L, B> K = make_cfg<C, L, B>();
+  constexpr SplitPlan<C, L, B> S{};
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t m[L];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; ++k) {
+    const int i0 = k < L ? 0 : k - L + 1, i1 = k < L ? k : L - 1;
+    if (!S.split[k]) {
+#pragma unroll
+      for (int i = i0; i <= i1; ++i) acc += (uint64_t)a[i] * b[k - i];
+#pragma unroll
+      for (int i = i0; i <= i1; ++i)
+        if (i < k || k >= L) acc += (uint64_t)m[i] * K.p[k - i];
+      if (k < L) {
+        m[k] = ((uint32_t)acc * K.inv) & MASK;
+        acc += (uint64_t)m[k] * K.p[0];
+      } else {
+        r[k - L] = (uint32_t)acc & MASK;
+      }
+      acc >>= B;
+    } else {
+      uint64_t s2 = 0;
+#pragma unroll
+      for (int i = i0; i <= i1; ++i) acc += (uint64_t)a[i] * b[k - i];
+#pragma unroll
+      for (int i = i0; i <= i1; ++i)
+        if (i < k || k >= L) s2 += (uint64_t)m[i] * K.p[k - i];
+      uint64_t lo = (uint64_t)(((uint32_t)acc & MASK) + ((uint32_t)s2 & MASK));
+      const uint64_t hi = (acc >> B) + (s2 >> B);
+      if (k < L) {
+        m[k] = ((uint32_t)lo * K.inv) & MASK;
+        lo += (uint64_t)m[k] * K.p[0];
+      } else {
+        r[k - L] = (uint32_t)lo & MASK;
+      }
+      acc = hi + (lo >> B);
+    }
+  }
+  r[L - 1] = (uint32_t)acc;
+}
+
 template <class C, int L, int B>
 __device__ void unpack(uint32_t* r, const Fe<C>& x) {
 #pragma unroll
@@ -130,7 +203,7 @@ __device__ Fe<C> dbl_n(Fe<C> x, int n) {
   return x;
 }
 
-template <class C, int L, int B>
+template <class C, int L, int B, bool SPLIT = false>
 __global__ void k_check(const Fe<C>* a, const Fe<C>* b, uint32_t n, uint32_t* bad) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
@@ -139,12 +212,13 @@ __global__ void k_check(const Fe<C>* a, const Fe<C>* b, uint32_t n, uint32_t* ba
   uint32_t ar[L], br[L], cr[L];
   unpack<C, L, B>(ar, dbl_n(a[t], SH));
   unpack<C, L, B>(br, dbl_n(b[t], SH));
-  red_mul<C, L, B>(cr, ar, br);
+  if (SPLIT) red_mul_split<C, L, B>(cr, ar, br);
+  else red_mul<C, L, B>(cr, ar, br);
   const Fe<C> got = pack_reduce<C, L, B>(cr);
   if (!fe_eq(got, dbl_n(c, SH))) atomicAdd(bad, 1u);
 }
 
-template <class C, int L, int B, int CHAINS>
+template <class C, int L, int B, int CHAINS, bool SPLIT = false>
 __global__ void __launch_bounds__(256) k_red_thr(uint32_t* io, uint32_t iters) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t x[CHAINS][L], y[L];
@@ -156,7 +230,10 @@ __global__ void __launch_bounds__(256) k_red_thr(uint32_t* io, uint32_t iters) {
     for (int i = 0; i < L; ++i) x[c][i] = y[i] ^ c;
   for (uint32_t it = 0; it < iters; ++it) {
 #pragma unroll
-    for (int c = 0; c < CHAINS; ++c) red_mul<C, L, B>(x[c], x[c], y);
+    for (int c = 0; c < CHAINS; ++c) {
+      if (SPLIT) red_mul_split<C, L, B>(x[c], x[c], y);
+      else red_mul<C, L, B>(x[c], x[c], y);
+    }
   }
 #pragma unroll
   for (int i = 0; i < L; ++i) {
@@ -195,7 +272,7 @@ static uint32_t rnd32() {
   return (uint32_t)(z ^ (z >> 31));
 }
 
-template <class C, int L, int B>
+template <class C, int L, int B, bool SPLIT = false>
 int check(const char* name) {
   const uint32_t n = 1 << 16;
   std::vector<Fe<C>> ha(n), hb(n);
@@ -225,7 +302,7 @@ int check(const char* name) {
   CHECK(hipMemset(dbad, 0, 4));
   CHECK(hipMemcpy(da, ha.data(), n * sizeof(Fe<C>), hipMemcpyHostToDevice));
   CHECK(hipMemcpy(db, hb.data(), n * sizeof(Fe<C>), hipMemcpyHostToDevice));
-  hipLaunchKernelGGL((k_check<C, L, B>), dim3(n / 256), dim3(256), 0, 0, da, db, n, dbad);
+  hipLaunchKernelGGL((k_check<C, L, B, SPLIT>), dim3(n / 256), dim3(256), 0, 0, da, db, n, dbad);
   uint32_t bad = 0;
   CHECK(hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost));
   std::printf("{\"test\":\"%s_check\",\"cases\":%u,\"mismatches\":%u}\n", name, n, bad);
@@ -235,7 +312,7 @@ int check(const char* name) {
   return bad != 0;
 }
 
-template <class C, int L, int B, int CHAINS>
+template <class C, int L, int B, int CHAINS, bool SPLIT = false>
 int thr(const char* name, uint32_t blocks, uint32_t iters) {
   const uint32_t total = blocks * 256;
   hipEvent_t e0, e1;
@@ -245,9 +322,9 @@ int thr(const char* name, uint32_t blocks, uint32_t iters) {
   uint32_t* io;
   CHECK(hipMalloc(&io, (size_t)total * L * 4));
   CHECK(hipMemset(io, 0x11, (size_t)total * L * 4));
-  hipLaunchKernelGGL((k_red_thr<C, L, B, CHAINS>), dim3(blocks), dim3(256), 0, 0, io, 4);
+  hipLaunchKernelGGL((k_red_thr<C, L, B, CHAINS, SPLIT>), dim3(blocks), dim3(256), 0, 0, io, 4);
   CHECK(hipEventRecord(e0));
-  hipLaunchKernelGGL((k_red_thr<C, L, B, CHAINS>), dim3(blocks), dim3(256), 0, 0, io, iters);
+  hipLaunchKernelGGL((k_red_thr<C, L, B, CHAINS, SPLIT>), dim3(blocks), dim3(256), 0, 0, io, iters);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   CHECK(hipEventElapsedTime(&ms, e0, e1));
@@ -275,7 +352,9 @@ int main() {
   int bad = 0;
   bad |= check<FpCfg, 14, 28>("fp14x28");
   bad |= check<FrCfg, 9, 29>("fr9x29");
+  bad |= check<FpCfg, 13, 30, true>("fp13x30split");
   thr<FpCfg, 14, 28, 2>("fp14x28", cus * 8, 256);
+  thr<FpCfg, 13, 30, 2, true>("fp13x30split", cus * 8, 256);
   thr<FrCfg, 9, 29, 4>("fr9x29", cus * 8, 512);
   return bad;
 }
