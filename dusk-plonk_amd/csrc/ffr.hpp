@@ -3,19 +3,26 @@
 // ff.hpp stores a field element as N packed 32-bit words and multiplies with a 96-bit
 // column accumulator: every 32x32 partial product costs v_mad_u64_u32 + v_addc (plus the
 // s_nop padding the compiler puts around inline asm). Here an element is L limbs of B < 32
-// bits (Fp: 14 x 28, Fr: 9 x 29) so that a whole product-scanning column — at most 2L
-// products below 2^(2B) plus the incoming carry — fits one 64-bit accumulator: ONE
-// v_mad_u64_u32 per partial product, no carry chain, plain C the scheduler can interleave.
-// Measured on MI355X (tools/ubench_limbs.hip): Fp 6.9e10 mul/s vs 4.8e10 packed, Fr 1.64e11
-// vs 1.09e11.
+// bits (Fp: 13 x 30, Fr: 9 x 29) so that each partial product is ONE v_mad_u64_u32 into a
+// 64-bit column accumulator, no carry chain, plain C the scheduler can interleave.
+// Fr (9 x 29): a whole product-scanning column — at most 2L products below 2^(2B) plus the
+// incoming carry — fits one accumulator. Fp (round 3: 13 x 30 instead of 14 x 28, 169 + 169
+// mads per product instead of 196 + 196): the middle columns' worst-case sums reach 2^64, so
+// those columns (RxPlan, computed at compile time from the limb bounds) keep the products and
+// the Montgomery reduction terms in separate accumulators and merge their low B bits and
+// carries — a few instructions per split column.
+// Measured on MI355X (tools/ubench_limbs.hip): Fp 13 x 30 7.86e10 mul/s vs 6.75e10 at
+// 14 x 28 and 4.8e10 packed; Fr 1.69e11 vs 1.09e11.
 //
-// Domain: Montgomery with R' = 2^(B*L) (Fp 2^392, Fr 2^261), values kept in [0, 2p) with
+// Domain: Montgomery with R' = 2^(B*L) (Fp 2^390, Fr 2^261), values kept in [0, 2p) with
 // normalised limbs (4p < R', so the product needs no final subtraction). Memory keeps the
 // packed layout of ff.hpp (2p < 2^(32N)): kernels unpack on load and pack on store, and a
 // buffer holds either R-domain (ff.hpp) or R'-domain values — each buffer's comment says
 // which. Conversion R -> R' is a multiplication by 2^(B*L - 32N) (doublings); R' -> R by
 // 2^-(B*L - 32N).
 #pragma once
+#include <type_traits>
+
 #include "ff.hpp"
 
 namespace plk {
@@ -24,10 +31,10 @@ template <class C>
 struct RxShape;
 template <>
 struct RxShape<FpCfg> {
-  static constexpr int L = 14, B = 28;
-  static constexpr uint32_t ONE[12] = {0x0347fcb8u, 0x19d80000u, 0x6d2002b1u, 0x12e00cdeu,
-                                       0xa2090c72u, 0x37669f83u, 0xda0f73e0u, 0x09b09b42u,
-                                       0x8f1297bbu, 0xa7c515d9u, 0xfcfa012cu, 0x0577a659u};  // 2^392 mod p
+  static constexpr int L = 13, B = 30;
+  static constexpr uint32_t ONE[12] = {0x00d1ff2eu, 0x46760000u, 0x9b4800acu, 0x84b80337u,
+                                       0xe882431cu, 0x0dd9a7e0u, 0xb683dcf8u, 0xc26c26d0u,
+                                       0x63c4a5eeu, 0x29f14576u, 0x7f3e804bu, 0x015de996u};  // 2^390 mod p
 };
 template <>
 struct RxShape<FrCfg> {
@@ -84,6 +91,47 @@ template <class C>
 struct RxK {
   static constexpr RxConst<C> k = rx_make<C>();
 };
+
+// Split-column plan of a Montgomery product with NPROD operand products (1: a*b or a^2,
+// 2: a*b + c*d) for shapes whose columns can overflow 64 bits (B >= 30). Operand limbs are
+// normalised (< 2^B) with a top limb below 2^(TOP_BITS) (values below 2^(B(L-1) + TOP_BITS):
+// every operand of the group law stays below 40p < 2^386, and the products' output bound
+// a b / R' + p < 2p already needs a b < 630 p^2 at R' = 2^390). split[k]: the worst-case sum
+// of column k (incoming carry + products + reduction terms m_i p_j) reaches 2^64, so the
+// products and the reduction terms (and for NPROD = 2 each product set) use separate
+// accumulators there. Every separate accumulator holds at most L products below 2^60 plus
+// the carry: below 2^64.
+template <class C>
+struct RxSplitOn {
+  static constexpr bool value = RxShape<C>::B >= 30;
+};
+
+template <class C, int NPROD>
+struct RxPlan {
+  static constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
+  static constexpr int TOP_BITS = 26;
+  bool split[2 * L - 1];
+  constexpr RxPlan() : split{} {
+    constexpr RxConst<C> K = RxK<C>::k;
+    long double carry = 0;
+    for (int k = 0; k < 2 * L - 1; ++k) {
+      long double sum = carry;
+      for (int i = 0; i < L; ++i) {
+        const int j = k - i;
+        if (j < 0 || j >= L) continue;
+        const long double ai = (long double)(1ull << (i == L - 1 ? TOP_BITS : B));
+        const long double bj = (long double)(1ull << (j == L - 1 ? TOP_BITS : B));
+        sum += NPROD * ai * bj + (long double)(1ull << B) * (long double)(K.p[j] + 1);
+      }
+      split[k] = sum >= 18446744073709551616.0L;  // 2^64 (exact worst case)
+      carry = sum / (long double)(1ull << B) + 4;
+    }
+  }
+};
+template <class C, int NPROD>
+struct RxPlanK {
+  static constexpr RxPlan<C, NPROD> k{};
+};
 // c*p as L limbs (c < 16). borrow_free: every limb below the top raised by 2^B - 1 (2^B for
 // limb 0) by borrowing from the limb above, so limbs 0..L-2 lie in [2^B - 1, 2^(B+1) - 1):
 // a_i + q_i - b_i >= 0 limb by limb for any normalised b whose top limb is below q's.
@@ -120,6 +168,39 @@ struct RxMultipleK {
 
 #define PLK_RX __device__ __forceinline__
 
+// Close column k of a split-capable product: acc holds the products (+ the incoming
+// carry), s2 the reduction terms and s3 a second product set (split columns only; both 0
+// otherwise). Below L the column's Montgomery digit m[k] is formed and its m_k p_0 added;
+// from L on the low B bits are output limb k - L. acc leaves holding the carry.
+template <class C>
+PLK_RX void rx_column_close(bool split, int k, uint64_t& acc, uint64_t s2, uint64_t s3,
+                            uint32_t* m, Rx<C>& r) {
+  constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  constexpr RxConst<C> K = RxK<C>::k;
+  if (!split) {
+    if (k < L) {
+      m[k] = ((uint32_t)acc * K.inv) & MASK;
+      acc += (uint64_t)m[k] * K.p[0];
+    } else {
+      r.v[k - L] = (uint32_t)acc & MASK;
+    }
+    acc >>= B;
+    return;
+  }
+  // low B bits of each part (< 3 * 2^B < 2^32) and their carries, summed apart
+  const uint32_t lo32 = ((uint32_t)acc & MASK) + ((uint32_t)s2 & MASK) + ((uint32_t)s3 & MASK);
+  const uint64_t hi = (acc >> B) + (s2 >> B) + (s3 >> B);
+  uint64_t lo = lo32;
+  if (k < L) {
+    m[k] = (lo32 * K.inv) & MASK;
+    lo += (uint64_t)m[k] * K.p[0];
+  } else {
+    r.v[k - L] = lo32 & MASK;
+  }
+  acc = hi + (lo >> B);
+}
+
 template <class C>
 PLK_RX Rx<C> rx_zero() {
   Rx<C> r;
@@ -146,24 +227,39 @@ PLK_RX Rx<C> rx_mul(const Rx<C>& a, const Rx<C>& b) {
   uint32_t m[L];
   Rx<C> r;
   uint64_t acc = 0;
+  if constexpr (!RxSplitOn<C>::value) {
 #pragma unroll
-  for (int k = 0; k < L; ++k) {
+    for (int k = 0; k < L; ++k) {
 #pragma unroll
-    for (int i = 0; i <= k; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+      for (int i = 0; i <= k; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
 #pragma unroll
-    for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * K.p[k - i];
-    m[k] = ((uint32_t)acc * K.inv) & MASK;
-    acc += (uint64_t)m[k] * K.p[0];
-    acc >>= B;
-  }
+      for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+      m[k] = ((uint32_t)acc * K.inv) & MASK;
+      acc += (uint64_t)m[k] * K.p[0];
+      acc >>= B;
+    }
 #pragma unroll
-  for (int k = L; k < 2 * L - 1; ++k) {
+    for (int k = L; k < 2 * L - 1; ++k) {
 #pragma unroll
-    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+      for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
 #pragma unroll
-    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)m[i] * K.p[k - i];
-    r.v[k - L] = (uint32_t)acc & MASK;
-    acc >>= B;
+      for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+      r.v[k - L] = (uint32_t)acc & MASK;
+      acc >>= B;
+    }
+  } else {
+    constexpr RxPlan<C, 1> PL = RxPlanK<C, 1>::k;
+#pragma unroll
+    for (int k = 0; k < 2 * L - 1; ++k) {
+      const int i0 = k < L ? 0 : k - L + 1, i1 = k < L ? k : L - 1;
+      uint64_t s2 = 0;
+#pragma unroll
+      for (int i = i0; i <= i1; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+#pragma unroll
+      for (int i = i0; i <= i1; ++i)
+        if (i < k || k >= L) (PL.split[k] ? s2 : acc) += (uint64_t)m[i] * K.p[k - i];
+      rx_column_close<C>(PL.split[k], k, acc, s2, 0, m, r);
+    }
   }
   r.v[L - 1] = (uint32_t)acc;
   return r;
@@ -171,7 +267,9 @@ PLK_RX Rx<C> rx_mul(const Rx<C>& a, const Rx<C>& b) {
 
 // (a*b + c*d) / R' mod p with ONE Montgomery reduction: both product columns accumulate
 // into the same 64-bit column (the caller bounds the limbs so that 2L products plus L
-// reduction products stay below 2^64, and the value so that (ab + cd) / R' + p < 2p).
+// reduction products stay below 2^64 — or, for split shapes, each product set and the
+// reduction terms in an accumulator of their own — and the value so that
+// (ab + cd) / R' + p < 2p).
 template <class C>
 PLK_RX Rx<C> rx_mul_add(const Rx<C>& a, const Rx<C>& b, const Rx<C>& c, const Rx<C>& d) {
   constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
@@ -180,28 +278,45 @@ PLK_RX Rx<C> rx_mul_add(const Rx<C>& a, const Rx<C>& b, const Rx<C>& c, const Rx
   uint32_t m[L];
   Rx<C> r;
   uint64_t acc = 0;
+  if constexpr (!RxSplitOn<C>::value) {
 #pragma unroll
-  for (int k = 0; k < L; ++k) {
+    for (int k = 0; k < L; ++k) {
 #pragma unroll
-    for (int i = 0; i <= k; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+      for (int i = 0; i <= k; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
 #pragma unroll
-    for (int i = 0; i <= k; ++i) acc += (uint64_t)c.v[i] * d.v[k - i];
+      for (int i = 0; i <= k; ++i) acc += (uint64_t)c.v[i] * d.v[k - i];
 #pragma unroll
-    for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * K.p[k - i];
-    m[k] = ((uint32_t)acc * K.inv) & MASK;
-    acc += (uint64_t)m[k] * K.p[0];
-    acc >>= B;
-  }
+      for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+      m[k] = ((uint32_t)acc * K.inv) & MASK;
+      acc += (uint64_t)m[k] * K.p[0];
+      acc >>= B;
+    }
 #pragma unroll
-  for (int k = L; k < 2 * L - 1; ++k) {
+    for (int k = L; k < 2 * L - 1; ++k) {
 #pragma unroll
-    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+      for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
 #pragma unroll
-    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)c.v[i] * d.v[k - i];
+      for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)c.v[i] * d.v[k - i];
 #pragma unroll
-    for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)m[i] * K.p[k - i];
-    r.v[k - L] = (uint32_t)acc & MASK;
-    acc >>= B;
+      for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+      r.v[k - L] = (uint32_t)acc & MASK;
+      acc >>= B;
+    }
+  } else {
+    constexpr RxPlan<C, 2> PL = RxPlanK<C, 2>::k;
+#pragma unroll
+    for (int k = 0; k < 2 * L - 1; ++k) {
+      const int i0 = k < L ? 0 : k - L + 1, i1 = k < L ? k : L - 1;
+      uint64_t s2 = 0, s3 = 0;
+#pragma unroll
+      for (int i = i0; i <= i1; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+#pragma unroll
+      for (int i = i0; i <= i1; ++i) (PL.split[k] ? s3 : acc) += (uint64_t)c.v[i] * d.v[k - i];
+#pragma unroll
+      for (int i = i0; i <= i1; ++i)
+        if (i < k || k >= L) (PL.split[k] ? s2 : acc) += (uint64_t)m[i] * K.p[k - i];
+      rx_column_close<C>(PL.split[k], k, acc, s2, s3, m, r);
+    }
   }
   r.v[L - 1] = (uint32_t)acc;
   return r;
@@ -218,22 +333,39 @@ PLK_RX Rx<C> rx_sqr(const Rx<C>& a) {
   for (int i = 0; i < L; ++i) a2[i] = a.v[i] << 1;
   Rx<C> r;
   uint64_t acc = 0;
+  if constexpr (!RxSplitOn<C>::value) {
 #pragma unroll
-  for (int k = 0; k < 2 * L - 1; ++k) {
+    for (int k = 0; k < 2 * L - 1; ++k) {
 #pragma unroll
-    for (int i = (k < L ? 0 : k - L + 1); 2 * i < k; ++i) acc += (uint64_t)a.v[i] * a2[k - i];
-    if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
-    if (k < L) {
+      for (int i = (k < L ? 0 : k - L + 1); 2 * i < k; ++i) acc += (uint64_t)a.v[i] * a2[k - i];
+      if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+      if (k < L) {
 #pragma unroll
-      for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * K.p[k - i];
-      m[k] = ((uint32_t)acc * K.inv) & MASK;
-      acc += (uint64_t)m[k] * K.p[0];
-    } else {
+        for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+        m[k] = ((uint32_t)acc * K.inv) & MASK;
+        acc += (uint64_t)m[k] * K.p[0];
+      } else {
 #pragma unroll
-      for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)m[i] * K.p[k - i];
-      r.v[k - L] = (uint32_t)acc & MASK;
+        for (int i = k - L + 1; i < L; ++i) acc += (uint64_t)m[i] * K.p[k - i];
+        r.v[k - L] = (uint32_t)acc & MASK;
+      }
+      acc >>= B;
     }
-    acc >>= B;
+  } else {
+    // the doubled cross products and the square sum to the product column of a * a
+    constexpr RxPlan<C, 1> PL = RxPlanK<C, 1>::k;
+#pragma unroll
+    for (int k = 0; k < 2 * L - 1; ++k) {
+      const int i0 = k < L ? 0 : k - L + 1, i1 = k < L ? k : L - 1;
+      uint64_t s2 = 0;
+#pragma unroll
+      for (int i = i0; 2 * i < k; ++i) acc += (uint64_t)a.v[i] * a2[k - i];
+      if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+#pragma unroll
+      for (int i = i0; i <= i1; ++i)
+        if (i < k || k >= L) (PL.split[k] ? s2 : acc) += (uint64_t)m[i] * K.p[k - i];
+      rx_column_close<C>(PL.split[k], k, acc, s2, 0, m, r);
+    }
   }
   r.v[L - 1] = (uint32_t)acc;
   return r;
@@ -322,19 +454,28 @@ PLK_RX Rx<C> rx_neg(const Rx<C>& a) {
 // ---- unnormalised differences (feed multiplications only) ---------------------------
 // a + c*p - b limb by limb, no carries: a normalised with value < 2p, b normalised with
 // value < (c - 1) p. Limbs < 2^(B+2) and value < (c + 2) p — rx_mul / rx_sqr accept such
-// operands (Fp: a 64-bit column of 14 products below 2^60 plus 14 reduction products below
-// 2^56 stays under 2^64; the output (12p)^2 / R' + p < 2p, normalised).
+// operands for shapes whose columns keep headroom (Fr 9 x 29: a 64-bit column of 9 products
+// below 2^61.6 plus 9 reduction products below 2^58 stays under 2^64). Split shapes (Fp
+// 13 x 30, RxPlan) assume normalised operand limbs: there the difference is carried
+// (rx_sub_n, same value range, ~2 more instructions per limb).
+template <class C, uint32_t CP>
+PLK_RX Rx<C> rx_sub_n(const Rx<C>& a, const Rx<C>& b);
+
 template <class C, uint32_t CP>
 PLK_RX Rx<C> rx_sub_u(const Rx<C>& a, const Rx<C>& b) {
-  constexpr RxMultiple<C> Q = RxMultipleK<C, CP, true>::k;
-  Rx<C> r;
+  if constexpr (RxSplitOn<C>::value) {
+    return rx_sub_n<C, CP>(a, b);
+  } else {
+    constexpr RxMultiple<C> Q = RxMultipleK<C, CP, true>::k;
+    Rx<C> r;
 #pragma unroll
-  for (int i = 0; i < RxShape<C>::L; ++i) r.v[i] = a.v[i] + Q.v[i] - b.v[i];
-  return r;
+    for (int i = 0; i < RxShape<C>::L; ++i) r.v[i] = a.v[i] + Q.v[i] - b.v[i];
+    return r;
+  }
 }
 
 // a + c*p - b with the carries propagated (signed): normalised limbs, value in
-// (c*p - max b, c*p + max a) — no conditional pass
+// (c*p - max b, c*p + max a) — no conditional pass. a, b normalised (a_i + (cp)_i < 2^31)
 template <class C, uint32_t CP>
 PLK_RX Rx<C> rx_sub_n(const Rx<C>& a, const Rx<C>& b) {
   constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
@@ -351,20 +492,37 @@ PLK_RX Rx<C> rx_sub_n(const Rx<C>& a, const Rx<C>& b) {
   return d;
 }
 
-// a + c*p - b - 2e, carries propagated (the X3 of the XYZZ addition in one pass)
+// a + c*p - b - 2e, carries propagated (the X3 of the XYZZ addition in one pass); 64-bit
+// limb sums where a limb of 2e can exceed 2^31 (B >= 30)
 template <class C, uint32_t CP>
 PLK_RX Rx<C> rx_sub2_n(const Rx<C>& a, const Rx<C>& b, const Rx<C>& e) {
   constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
   constexpr uint32_t MASK = (1u << B) - 1;
   constexpr RxMultiple<C> Q = RxMultipleK<C, CP, false>::k;
+  using S = typename std::conditional<(B >= 30), int64_t, int32_t>::type;
   Rx<C> d;
-  int32_t c = 0;
+  S c = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    const int32_t t =
-        (int32_t)(a.v[i] + Q.v[i]) - (int32_t)b.v[i] - (int32_t)(e.v[i] << 1) + c;
+    const S t = (S)(a.v[i] + Q.v[i]) - (S)b.v[i] - ((S)e.v[i] << 1) + c;
     d.v[i] = i == L - 1 ? (uint32_t)t : ((uint32_t)t & MASK);
     c = t >> B;
+  }
+  return d;
+}
+
+// k * a (k small) with the carries propagated: normalised limbs, value k * a
+template <class C, uint32_t KM>
+PLK_RX Rx<C> rx_small_mul_n(const Rx<C>& a) {
+  constexpr int L = RxShape<C>::L, B = RxShape<C>::B;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  Rx<C> d;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const uint64_t t = (uint64_t)a.v[i] * KM + c;
+    d.v[i] = i == L - 1 ? (uint32_t)t : ((uint32_t)t & MASK);
+    c = (uint32_t)(t >> B);
   }
   return d;
 }

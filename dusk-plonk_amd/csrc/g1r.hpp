@@ -142,9 +142,9 @@ __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, con
   const RFp Q = rx_mul(p.X, PP);
   G1R r;
   r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
-  // Y3 = R (Q - X3) + (5p - Y1) PPP with one reduction: limbs of R, Q - X3 + 10p below
-  // 3*2^28, of 5p - Y1 below 2^29, PPP normalised -> columns < 168 * 2^56 < 2^64; value
-  // (8p * 12p + 5p * 2p) / R' + p < 1.06p
+  // Y3 = R (Q - X3) + (5p - Y1) PPP with one reduction (all operands normalised, the
+  // split columns of rx_mul_add keep each accumulator below 2^64); value
+  // (8p * 12p + 5p * 2p) / R' + p < 2p at R' = 2^390
   r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP);
   r.ZZ = rx_mul(p.ZZ, PP);
   r.ZZZ = rx_mul(p.ZZZ, PPP);
@@ -175,7 +175,8 @@ __device__ __forceinline__ G1R g1r_madd_lazy(const G1R& p, const RFp& x2, const 
   return r;
 }
 
-// 4p - y, unnormalised (limbs < 2^(B+1) + 2^B): the negated affine y for g1r_madd_lazy
+// 4p - y (normalised for the split Fp shape, rx_sub_u): the negated affine y for
+// g1r_madd_lazy
 __device__ __forceinline__ RFp rx_neg_lazy(const RFp& y) { return rx_sub_u<FpCfg, 4>(rx_zero<FpCfg>(), y); }
 
 __device__ __forceinline__ G1R g1r_lazy_finish(const G1R& p) {
@@ -215,19 +216,16 @@ __device__ __forceinline__ G1R g1r_add_lazy_sl(const G1R& p, const G1R& q) {
 // lazy normalisation of g1r_madd_lazy_sl: result X3 in (2p, 8p), Y3 < 2p. Infinity (ZZ = 0)
 // stays infinity (ZZ3 = V ZZ); G1 has no 2-torsion, so Y != 0 otherwise.
 __device__ __forceinline__ G1R g1r_dbl_lazy(const G1R& p) {
-  RFp U, M;
-#pragma unroll
-  for (int i = 0; i < RxShape<FpCfg>::L; ++i) U.v[i] = p.Y.v[i] << 1;  // 2Y < 8p, limbs < 2^29
+  const RFp U = rx_small_mul_n<FpCfg, 2>(p.Y);  // 2Y < 8p, normalised
   const RFp V = rx_sqr(U);
   const RFp W = rx_mul(U, V);
   const RFp S = rx_mul(p.X, V);
   const RFp X2 = rx_sqr(p.X);
-#pragma unroll
-  for (int i = 0; i < RxShape<FpCfg>::L; ++i) M.v[i] = X2.v[i] * 3u;  // 3X^2 < 6p, limbs < 2^30
+  const RFp M = rx_small_mul_n<FpCfg, 3>(X2);  // 3X^2 < 6p, normalised
   G1R r;
   r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(M), rx_zero<FpCfg>(), S);  // M^2 + 6p - 2S in (2p, 8p)
-  // Y3 = M (S - X3) - W Y = M (S - X3 + 10p) + (5p - Y) W, one reduction (bounds as in
-  // g1r_madd_lazy_sl: M limbs < 3 * 2^28, value < 6p)
+  // Y3 = M (S - X3) - W Y = M (S - X3 + 10p) + (5p - Y) W, one reduction (value
+  // (6p * 12p + 5p * 2p) / R' + p < 2p)
   r.Y = rx_mul_add(M, rx_sub_u<FpCfg, 10>(S, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), W);
   r.ZZ = rx_mul(V, p.ZZ);
   r.ZZZ = rx_mul(W, p.ZZZ);

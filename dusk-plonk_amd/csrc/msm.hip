@@ -845,12 +845,14 @@ __global__ void k_any_nonzero(MsmBatch batch, uint32_t* __restrict__ flag) {
 
 }  // namespace
 
-// R'-domain [0, 2p) packed coordinates (ffr.hpp) -> canonical R-domain: x * 2^-8 with the
-// R-domain product x * 2^376 / 2^384.
+// R'-domain [0, 2p) packed coordinates (ffr.hpp) -> canonical R-domain: x * 2^-SH
+// (SH = BL - 384 = 6) as the R-domain product x * 2^(384 - SH) / 2^384.
 static Fp fp_rx_to_r(Fp x) {
+  constexpr int SH = RxShape<FpCfg>::B * RxShape<FpCfg>::L - 32 * FpCfg::N;
+  static_assert(SH > 0 && SH < 32, "R' / R shift");
   fe_reduce_once(x);
   Fp k = fe_zero<FpCfg>();
-  k.v[11] = 0x01000000u;  // 2^376 (< p)
+  k.v[11] = 1u << (32 - SH);  // 2^(384 - SH) (< p)
   return fe_mul(x, k);
 }
 static G1xyzz rx_to_r_domain(const G1xyzz& p) {
