@@ -40,6 +40,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # peak; this one is MEASURED by tools/ubench_mad.hip (3.53e13/s chip-wide at 4 waves/SIMD,
 # 3.2e13 at 2; dependent latency = issue cost).
 VALU_MAD_PEAK = 3.53e13
+# The VALU issue ceiling: every SIMD issuing every cycle at the chip's max clock
+# (MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2400 MHz). A loop's demand is its compiled
+# instruction mix priced at the measured issue cost of each instruction (tools/ubench_issue.hip,
+# profiles/r03_ubench_issue.txt: 64-bit ops and v_mad_u64_u32 ~4.3-4.5 cycles, 32-bit ALU ~2.3).
+SIMD_CYCLES_PEAK = 1024 * 2.4e9
 FR_MUL_PEAK = 1.64e11  # ffr.hpp Fr multiplies/s chip-wide, tools/ubench_limbs.hip (measured)
 VALU_MAD_PEAK_SOURCE = ("measured by tools/ubench_mad.hip (independent v_mad_u64_u32 chains, "
                         "4 waves/SIMD, whole chip); MI355X_MICROARCH.md lists no integer-mad peak")
@@ -51,8 +56,9 @@ _ISA = {}
 
 
 def compiled_loop(kernel: str = "k_accumulateILb0E") -> dict:
-    """v_mad_u64_u32 / instructions of the kernel's loop body as compiled (largest basic
-    block of its gfx950 code in libplk.so, tools/isa_count.py)."""
+    """The kernel's loop body as compiled (largest basic block of its gfx950 code in
+    libplk.so, tools/isa_count.py): v_mad_u64_u32 count, instruction count and the VALU issue
+    cycles of the mix at the measured per-instruction costs (tools/ubench_issue.hip)."""
     if kernel not in _ISA:
         try:
             sys.path.insert(0, str(ROOT / "tools"))
@@ -60,13 +66,16 @@ def compiled_loop(kernel: str = "k_accumulateILb0E") -> dict:
             lib = os.environ.get("PLK_LIB") or str(ROOT / "dusk-plonk_amd" / "libplk.so")
             r = isa_count.largest_block(Path(lib), kernel)
             _ISA[kernel] = ({"v_mad_u64_u32": r["v_mad_u64_u32"], "instructions": r["instructions"],
+                             "valu_cycles": isa_count.valu_cycles(r["mix"]),
                              "source": "compiled loop body (tools/isa_count.py on libplk.so)"}
                             if r else None)
         except Exception as e:  # noqa: BLE001 — llvm-objdump missing: formula fallback
             _ISA[kernel] = {"v_mad_u64_u32": MADS_PER_MIXED_ADD, "instructions": None,
+                            "valu_cycles": MADS_PER_MIXED_ADD * 4.53 * 1.3,
                             "source": f"formula (compiled count unavailable: {e!r})"}
         if _ISA[kernel] is None:
             _ISA[kernel] = {"v_mad_u64_u32": MADS_PER_MIXED_ADD, "instructions": None,
+                            "valu_cycles": MADS_PER_MIXED_ADD * 4.53 * 1.3,
                             "source": "formula (kernel not found in libplk.so)"}
     return _ISA[kernel]
 
@@ -453,26 +462,35 @@ def host_info():
 
 
 def valu_roofline(adds_per_s):
-    """k_accumulate against its binding ceiling: v_mad_u64_u32 issue (mads/s), with the mads
-    per mixed addition counted in the compiled loop."""
+    """k_accumulate against its binding ceiling, VALU issue: each mixed addition's compiled
+    instruction mix priced at the measured per-instruction issue costs, per wave of 64
+    additions, against every SIMD issuing every cycle (SIMD-cycles/s). The v_mad_u64_u32 rate
+    against its own measured peak is kept beside it."""
     isa = compiled_loop()
-    achieved = adds_per_s * isa["v_mad_u64_u32"]
-    return {"bound": "valu", "achieved": achieved, "peak": VALU_MAD_PEAK, "unit": "mad/s",
-            "frac": achieved / VALU_MAD_PEAK, "peak_source": VALU_MAD_PEAK_SOURCE,
+    achieved = adds_per_s / 64.0 * isa["valu_cycles"]
+    mads = adds_per_s * isa["v_mad_u64_u32"]
+    return {"bound": "valu", "achieved": achieved, "peak": SIMD_CYCLES_PEAK,
+            "unit": "SIMD issue-cycles/s", "frac": achieved / SIMD_CYCLES_PEAK,
+            "peak_source": "1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md); per-instruction issue "
+                           "costs measured by tools/ubench_issue.hip (profiles/r03_ubench_issue.txt)",
+            "valu_cycles_per_wave_of_adds": isa["valu_cycles"],
             "mads_per_point_add": isa["v_mad_u64_u32"],
-            "instructions_per_point_add": isa["instructions"], "mads_source": isa["source"]}
+            "instructions_per_point_add": isa["instructions"], "mads_source": isa["source"],
+            "mad": {"achieved": mads, "peak": VALU_MAD_PEAK, "unit": "mad/s",
+                    "frac": mads / VALU_MAD_PEAK, "peak_source": VALU_MAD_PEAK_SOURCE}}
 
 
 def binding_roofline(valu: dict, hbm_achieved_gbs: float, alg_bytes: float, traffic,
                      kernel: str) -> dict:
-    """The roofline object of the bench line: the BINDING (integer-VALU) roofline at top level
-    (bound / achieved / peak / frac), HBM as the required secondary figure under `hbm`, and
-    `traffic` = PMC-measured HBM bytes per launch."""
+    """The roofline object of the bench line: the BINDING (integer-VALU issue) roofline at top
+    level (bound / achieved / peak / frac), HBM as the required secondary figure under `hbm`,
+    and `traffic` = PMC-measured HBM bytes per launch."""
     return {"bound": "valu", "kernel": kernel, "achieved": valu["achieved"], "peak": valu["peak"],
-            "unit": "mad/s", "frac": valu["frac"], "peak_source": valu["peak_source"],
+            "unit": valu["unit"], "frac": valu["frac"], "peak_source": valu["peak_source"],
+            "valu_cycles_per_wave_of_adds": valu["valu_cycles_per_wave_of_adds"],
             "mads_per_point_add": valu["mads_per_point_add"],
             "instructions_per_point_add": valu["instructions_per_point_add"],
-            "mads_source": valu["mads_source"], "traffic": traffic,
+            "mads_source": valu["mads_source"], "mad": valu["mad"], "traffic": traffic,
             "hbm": {"achieved": hbm_achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm_achieved_gbs / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": alg_bytes,
@@ -658,9 +676,10 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
             "point_adds_per_launch": solo["point_adds_per_launch"],
             "point_adds_per_s": solo["point_adds_per_s"],
             "solo": solo, "in_workload": inw,
-            "note": "integer-VALU-bound (no MFMA): frac = v_mad_u64_u32 issue of the solo "
-                    "launches against the measured mad peak; HBM under `hbm` (4 commit batches "
-                    "per proof: 4, 1, 4 and 2 MSMs)",
+            "note": "integer-VALU-bound (no MFMA): frac = VALU issue cycles of the solo launches' "
+                    "mixed additions (compiled mix x measured costs) over every SIMD issuing every "
+                    "cycle at 2.4 GHz; HBM under `hbm` (4 commit batches per proof: 4, 1, 4 and "
+                    "2 MSMs)",
         })
         result["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -80,6 +80,7 @@ def test_compiled_loop_mads():
     isa = bench.compiled_loop()
     assert "compiled" in isa["source"], isa
     assert 3000 < isa["v_mad_u64_u32"] < isa["instructions"] < 6000
+    assert isa["v_mad_u64_u32"] * 4 < isa["valu_cycles"] < isa["instructions"] * 5
 
 
 def test_gpus_flag_must_match_launcher():
@@ -99,7 +100,7 @@ def test_prove_mode_line_has_solo_roofline():
     assert r["avg_launch_ms"] == r["solo"]["avg_launch_ms"]
     assert r["in_workload"]["launches"] == 2 * 2 * 4
     # the binding roofline at top level, HBM as the secondary figure
-    assert r["bound"] == "valu" and r["unit"] == "mad/s" and r["hbm"]["unit"] == "GB/s"
+    assert r["bound"] == "valu" and r["hbm"]["unit"] == "GB/s" and r["mad"]["unit"] == "mad/s"
     assert r["mads_per_point_add"] > 3000 and "compiled" in r["mads_source"]
     assert "13 transforms" in d["config"]["workload"] and "1 public input" in d["config"]["workload"]
 

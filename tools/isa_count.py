@@ -92,7 +92,7 @@ def largest_block(lib: Path, pat: str) -> dict | None:
                 _, c = max(blocks, key=lambda b: sum(b[1].values()))
                 return {"kernel": pat, "instructions": sum(c.values()),
                         "v_mad_u64_u32": sum(v for k, v in c.items() if k.startswith("v_mad_u64_u32")),
-                        "top": c.most_common(8)}
+                        "top": c.most_common(8), "mix": dict(c)}
     return None
 
 
@@ -100,3 +100,25 @@ if __name__ == "__main__":
     lib = Path(sys.argv[1]) if len(sys.argv) > 1 else ROOT / "dusk-plonk_amd" / "libplk.so"
     pat = sys.argv[2] if len(sys.argv) > 2 else "k_accumulateILb0E"
     print(largest_block(lib, pat))
+
+
+# Issue cost of a VALU wave-instruction on one SIMD, in cycles, measured chip-wide at 4 waves
+# per SIMD (tools/ubench_issue.hip, profiles/r03_ubench_issue.txt): 64-bit and 32-bit
+# multiply forms issue at about half the rate of 32-bit integer ALU instructions.
+ISSUE_CYCLES = {"v_mad_u64_u32": 4.53, "v_lshrrev_b64": 4.24, "v_lshlrev_b64": 4.24,
+                "v_ashrrev_i64": 4.24, "v_lshl_add_u64": 4.36, "v_mul_lo_u32": 4.26,
+                "v_mul_hi_u32": 4.26}
+ISSUE_CYCLES_VALU32 = 2.30  # v_and / v_add / v_ashrrev measured 2.29-2.32
+
+
+def valu_cycles(mix: dict) -> float:
+    """SIMD issue cycles of one pass of a block with opcode counts `mix`: VALU instructions at
+    their measured costs (prefix match on the mnemonic, e.g. v_add_u32_e32), scalar, memory and
+    LDS instructions excluded (they issue on other units)."""
+    cyc = 0.0
+    for op, n in mix.items():
+        if not op.startswith("v_"):
+            continue
+        base = next((c for k, c in ISSUE_CYCLES.items() if op.startswith(k)), ISSUE_CYCLES_VALU32)
+        cyc += n * base
+    return cyc
