@@ -306,10 +306,20 @@ __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
 constexpr uint32_t kFineBits = 10;
 constexpr uint32_t kFine = 1u << kFineBits;  // buckets per coarse bin = threads of k_fine
 constexpr uint32_t kCoarseMax = 4096;        // coarse bins (B <= 2^22, c <= 23)
-// bucket reduction: runs of 2^rb buckets per lane, rb = kRunBits (16) for batches of several
-// MSMs; a lone MSM takes kRunBitsLone (8): twice the lanes, half the chain per lane (its
-// run-sum kernels are latency-bound on half the chip otherwise)
-constexpr uint32_t kRunBits = 4, kRunBitsLone = 3;
+// bucket reduction: runs of K = 2^rb buckets per lane. Batches of several MSMs (the
+// prover's commit groups, with other proofs' kernels beside them) take 16. A lone MSM's
+// run-sum chains are latency-bound with the chip otherwise idle, so its rb is the largest
+// rb <= kRunBits that still gives kRunLanes run lanes: 4 at 2^20 (round 2: a fixed 8), 2 at
+// 2^16 (lone 2^16 MSM 1.14 -> 1.01 ms). Applied to batches too it cost the 2^16 proof
+// 22 -> 18 M constraints/s (more bit-sum groups, NR / 256, in every commit group).
+constexpr uint32_t kRunBits = 4, kRunBitsMin = 1;
+constexpr size_t kRunLanes = 131072;  // two waves per SIMD of the run-sum kernels
+inline uint32_t run_bits(uint32_t B, uint32_t slots) {
+  if (slots > 1) return kRunBits;
+  uint32_t rb = kRunBits;
+  while (rb > kRunBitsMin && (size_t)(B >> rb) < kRunLanes) --rb;
+  return rb;
+}
 
 // Exclusive scan over the workgroup of K values per thread (wave shuffles, then the wave
 // totals through LDS); tot = the workgroup totals. sh: K * 32 words.
@@ -798,11 +808,17 @@ __global__ void __launch_bounds__(Z ? 384 : 256) k_bitsum1(uint32_t B, const G1x
 // Workgroup j of slot: T_j = sum_g T_j(g) for 0 < j < 8; T_0 = sum_g (T_0(g) + A_g);
 // T_(8+i) = sum_(g: bit i of g) A_g; wide bucket sets: j = nbits sum_g of the plain sums,
 // j = nbits + 1 sum_g A_g.
+// Also the batch's readback record (ReadbackHeader): workgroup (0, slot) copies the slot's
+// entry count (its point additions, offsets[B]) next to the flags k_any_nonzero stamped, so
+// the host reads flags, counts and bit sums with ONE copy.
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, uint32_t nout,
-                                                 G1xyzz* __restrict__ out) {
+                                                 G1xyzz* __restrict__ out,
+                                                 const uint32_t* __restrict__ offsets, uint32_t B,
+                                                 uint32_t* __restrict__ entries) {
   __shared__ G1xyzz sh[4];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
+  if (j == 0 && tid == 0) entries[slot] = offsets[(size_t)slot * (B + 1) + B];
   in += (size_t)slot * G * kBitsumOut;
   G1R acc = g1r_infinity();
   for (uint32_t g = tid; g < G; g += 256) {
@@ -829,18 +845,28 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
   const uint32_t nw = min(G, 256u) > 64 ? min(G, 256u) >> 6 : 1;  // waves holding values
   if ((tid & 63) == 0 && (tid >> 6) < nw) st_g1r(&sh[tid >> 6], acc);
   __syncthreads();
-  if (tid == 0) {
-    for (uint32_t w = 1; w < nw; ++w) acc = g1r_add(acc, ld_g1r(&sh[w]));
-    st_g1r(&out[(size_t)slot * nout + j], acc);
+  if (tid < 2) {  // the (up to) 4 wave totals as a 2-level tree: lanes 0 / 1 add a pair each
+    acc = 2 * tid < nw ? ld_g1r(&sh[2 * tid]) : g1r_infinity();
+    if (2 * tid + 1 < nw) acc = g1r_add(acc, ld_g1r(&sh[2 * tid + 1]));
+  }
+  if (tid < 64) {  // wave 0 whole: the shuffle reads lane 1
+    G1R o;
+    o.X = shfl_down_rfp(acc.X, 1);
+    o.Y = shfl_down_rfp(acc.Y, 1);
+    o.ZZ = shfl_down_rfp(acc.ZZ, 1);
+    o.ZZZ = shfl_down_rfp(acc.ZZZ, 1);
+    if (tid == 0) st_g1r(&out[(size_t)slot * nout + j], nw > 2 ? g1r_add(acc, o) : acc);
   }
 }
 
-// flag[slot] |= any nonzero scalar in [len, check_len)  (commit degree check)
-__global__ void k_any_nonzero(MsmBatch batch, uint32_t* __restrict__ flag) {
+// flag[slot] = gen if any scalar in [len, check_len) is nonzero (commit degree check). The
+// flags are stamped with the batch's generation number instead of being cleared per batch:
+// a stale flag holds an older (smaller) generation, so no memset dispatch is needed.
+__global__ void k_any_nonzero(MsmBatch batch, uint32_t* __restrict__ flag, uint32_t gen) {
   const uint32_t slot = blockIdx.y;
   const uint64_t i = (uint64_t)batch.len[slot] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= batch.check_len[slot]) return;
-  if (!fe_is_zero(ld_fr(&batch.scalars[slot][i]))) atomicOr(&flag[slot], 1u);
+  if (!fe_is_zero(ld_fr(&batch.scalars[slot][i]))) atomicMax(&flag[slot], gen);
 }
 
 }  // namespace
@@ -864,7 +890,7 @@ static G1xyzz rx_to_r_domain(const G1xyzz& p) {
   return r;
 }
 
-int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
+int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStream_t stream) {
   const bool same_shape = w.cap_c == s->c && w.cap_windows == s->windows;
   if (same_shape && len <= w.cap_len && slots <= w.cap_slots && w.cap_len) return PLK_OK;
   // buffers only ever grow (DevBuf::alloc), so re-sizing for another shape keeps the larger
@@ -873,11 +899,14 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
   slots = std::max(slots, w.cap_slots);
   const size_t B = (size_t)1 << (s->c - 1);
   const bool wide = B > kLdsBuckets;
-  const size_t NC = B >> kFineBits, NR = B >> kRunBitsLone;  // the most runs
+  const size_t NC = B >> kFineBits;
+  // runs over all slots of a batch (run_bits: a batch runs B >> kRunBits per slot, a lone
+  // MSM fewer than 2 kRunLanes unless rb = kRunBits)
+  const size_t max_runs = std::max<size_t>(slots * (B >> kRunBits), 2 * kRunLanes);
   if (wide && NC > kCoarseMax) return PLK_E_ARG;
   const size_t entries = (size_t)s->windows * len;
   const size_t max_tasks = entries / kChunkMin + B + 1;
-  const size_t G = ((wide ? NR : B) + 255) / 256;
+  const size_t groups = wide ? (max_runs + 255) / 256 : slots * ((B + 255) / 256);
   if (max_tasks >= ((size_t)1 << kTaskShift)) return PLK_E_ARG;  // task records: partial index bits
   int st;
   const size_t hb = wide ? NC : B;  // histogram bins: coarse bins or buckets
@@ -897,14 +926,21 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots) {
     if ((st = w.len_fill.alloc(slots * kChunkMax * 4))) return st;
     if ((st = w.coarse_off.alloc(slots * (NC + 1) * 4))) return st;
     if ((st = w.rsum.alloc(slots * B * sizeof(G1xyzz)))) return st;
-    if ((st = w.ys.alloc(slots * NR * sizeof(G1xyzz)))) return st;
-    if ((st = w.zs.alloc(slots * NR * sizeof(G1xyzz)))) return st;
+    if ((st = w.ys.alloc(max_runs * sizeof(G1xyzz)))) return st;
+    if ((st = w.zs.alloc(max_runs * sizeof(G1xyzz)))) return st;
   } else {
     if ((st = w.bsum.alloc(slots * B * sizeof(G1xyzz)))) return st;
   }
-  if ((st = w.bits1.alloc(slots * G * kBitsumOut * sizeof(G1xyzz)))) return st;
-  if ((st = w.bits2.alloc(slots * 32 * sizeof(G1xyzz)))) return st;  // nbits <= 32
-  if ((st = w.flag.alloc(slots * 4 + 16))) return st;
+  if ((st = w.bits1.alloc(groups * kBitsumOut * sizeof(G1xyzz)))) return st;
+  {  // readback record: header (flags, entry counts) then the bit sums (nout <= 32 per slot)
+    void* before = w.bits2.ptr;
+    if ((st = w.bits2.alloc(sizeof(ReadbackHeader) + (size_t)kMaxSlots * 32 * sizeof(G1xyzz))))
+      return st;
+    if (w.bits2.ptr != before) {  // fresh memory: the flags start at generation 0
+      PLK_HIP_TRY(hipMemsetAsync(w.bits2.ptr, 0, sizeof(ReadbackHeader), stream));
+      w.gen = 0;
+    }
+  }
   if (!w.ev0) PLK_HIP_TRY(hipEventCreate(&w.ev0));
   if (!w.ev1) PLK_HIP_TRY(hipEventCreate(&w.ev1));
   const int lds = (int)(std::min<uint32_t>((uint32_t)B, kLdsBuckets) * 4);
@@ -943,13 +979,13 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     total_entries += (size_t)s->windows * lens[k];
   }
   int st;
-  if ((st = ws_reserve(s, w, max_len ? max_len : 1, (uint32_t)count))) return st;
+  if ((st = ws_reserve(s, w, max_len ? max_len : 1, (uint32_t)count, stream))) return st;
   const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1)};
   const uint32_t B = cfg.B;
   // wide bucket sets: two-level sort and run-sum reduction; the bit sums then run over the
   // NR = B / 2^rb runs instead of the buckets
   const bool wide = B > kLdsBuckets;
-  const uint32_t rb = count == 1 ? kRunBitsLone : kRunBits;
+  const uint32_t rb = run_bits(B, (uint32_t)count);
   const uint32_t NC = B >> kFineBits, NR = B >> rb;
   const uint32_t G = cdiv(wide ? NR : B, 256);  // a power of two
   const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
@@ -968,10 +1004,16 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   const uint32_t hist_blocks =
       std::max<uint32_t>(1, std::min<uint32_t>(kHistBlocksMax, cdiv(max_len, 512)));
 
-  PLK_HIP_TRY(hipMemsetAsync(w.flag.ptr, 0, slots * 4, stream));
+  ReadbackHeader* hdr_dev = w.bits2.as<ReadbackHeader>();
+  G1xyzz* bits_dev = reinterpret_cast<G1xyzz*>(hdr_dev + 1);
+  if (++w.gen == 0xFFFFFFFFu) {  // wrap: clear the stamps once every 2^32 - 1 batches
+    PLK_HIP_TRY(hipMemsetAsync(hdr_dev, 0, sizeof(ReadbackHeader), stream));
+    w.gen = 1;
+  }
+  const uint32_t gen = w.gen;
   if (max_tail) {
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
-                       batch, w.flag.as<uint32_t>());
+                       batch, hdr_dev->flag, gen);
   }
   if (wide) {
     PLK_HIP_TRY(hipMemsetAsync(w.len_cur.ptr, 0, (size_t)slots * kChunkMax * 4, stream));
@@ -1072,20 +1114,21 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        w.bits1.as<G1xyzz>());
   }
   hipLaunchKernelGGL(k_bitsum2, dim3(nout, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
-                     G, nbits, nout, w.bits2.as<G1xyzz>());
+                     G, nbits, nout, bits_dev, (const uint32_t*)w.offsets.as<uint32_t>(), B,
+                     hdr_dev->entries);
   PLK_HIP_TRY(hipGetLastError());
 
+  // ONE copy of the readback record: flags, entry counts, then the slots' bit sums
   const size_t t_count = (size_t)slots * nout;
-  if ((st = w.host_out.alloc(t_count * sizeof(G1xyzz) + 2 * slots * sizeof(uint32_t)))) return st;
-  G1xyzz* T = w.host_out.as<G1xyzz>();
-  uint32_t* flag = reinterpret_cast<uint32_t*>(T + t_count);
-  uint32_t* ent = flag + slots;
-  PLK_HIP_TRY(hipMemcpy2DAsync(ent, 4, w.offsets.as<uint32_t>() + B, (B + 1) * 4, 4, slots,
-                               hipMemcpyDeviceToHost, stream));
-  PLK_HIP_TRY(hipMemcpyAsync(T, w.bits2.ptr, t_count * sizeof(G1xyzz), hipMemcpyDeviceToHost,
-                             stream));
-  PLK_HIP_TRY(hipMemcpyAsync(flag, w.flag.ptr, slots * 4, hipMemcpyDeviceToHost, stream));
+  const size_t rec_bytes = sizeof(ReadbackHeader) + t_count * sizeof(G1xyzz);
+  if ((st = w.host_out.alloc(rec_bytes))) return st;
+  const ReadbackHeader* hdr = w.host_out.as<ReadbackHeader>();
+  const G1xyzz* T = reinterpret_cast<const G1xyzz*>(hdr + 1);
+  PLK_HIP_TRY(hipMemcpyAsync(w.host_out.ptr, hdr_dev, rec_bytes, hipMemcpyDeviceToHost, stream));
   PLK_HIP_TRY(stream_wait(stream));
+  const uint32_t* ent = hdr->entries;
+  uint32_t flag[kMaxSlots];
+  for (uint32_t k = 0; k < slots; ++k) flag[k] = hdr->flag[k] == gen ? 1u : 0u;
   MsmStats& stt = w.stats;
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, w.ev0, w.ev1) == hipSuccess) stt.last_accumulate_ms = ms;

@@ -73,12 +73,23 @@ __device__ __forceinline__ Fr ld_fr(const Fr* p) {
 
 inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+// Head of a batch's readback record (device buffer MsmWorkspace::bits2, copied to the host
+// in one piece with the bit sums that follow it): per slot the degree-check flag (stamped
+// with the batch's generation number by k_any_nonzero) and the entry count (point
+// additions, written by k_bitsum2). 128 bytes, so the G1xyzz records after it stay aligned.
+struct ReadbackHeader {
+  uint32_t flag[kMaxSlots];
+  uint32_t entries[kMaxSlots];
+};
+static_assert(sizeof(ReadbackHeader) % 16 == 0, "alignment of the bit sums");
+
 struct MsmWorkspace {
   DevBuf counts, blockhist, offsets, task_off, full_off, len_cur, sorted, tasks, partials, bsum, bits1,
-      bits2, flag;
+      bits2;
   // wide bucket sets only (msm.hip: two-level sort, run-sum reduction)
   DevBuf tmp, task_rel, bin_tot, len_fill, coarse_off, rsum, ys, zs;
-  PinnedBuf host_out;  // per-slot bit sums T, flags and entry counts read back by the host
+  PinnedBuf host_out;  // the readback record (ReadbackHeader + bit sums) on the host
+  uint32_t gen = 0;    // generation number of the last batch (degree-check flag stamps)
   size_t cap_len = 0, task_stride = 0, sorted_stride = 0;
   uint32_t cap_slots = 0;
   // the SRS shape the buffers and strides were sized for: a workspace moves between SRSs
@@ -93,6 +104,6 @@ struct MsmWorkspace {
   }
 };
 
-int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots);
+int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStream_t stream);
 
 }  // namespace plk

@@ -14,6 +14,8 @@
 // (or n^-1 g^-e) post-scale into the last pass' stores.
 //
 // HBM traffic per transform: P * 2 * N * 32 B (P = 3 at N = 2^20..2^24).
+#include <cstdlib>
+
 #include "ffr.hpp"
 #include "internal.hpp"
 
@@ -474,9 +476,15 @@ static void plan_domain(plk_domain* d) {
   const uint32_t L = d->log_n;
   d->plan.clear();
   if (L == 0) return;
-  // elements per workgroup: keep >= ~256 workgroups when the transform allows it
+  // elements per workgroup: keep >= ~256 workgroups when the transform allows it, and at
+  // least 2^PLK_NTT_LE_MIN (experiments; default 2^6)
+  static const uint32_t le_min = [] {
+    const char* e = getenv("PLK_NTT_LE_MIN");
+    const int v = e ? atoi(e) : 6;
+    return (uint32_t)(v >= 1 && v <= (int)kMaxLe ? v : 6);
+  }();
   uint32_t le = L > 8 ? L - 8 : 1;
-  if (le < 6) le = L < 6 ? L : 6;
+  if (le < le_min) le = L < le_min ? L : le_min;
   if (le > kMaxLe) le = kMaxLe;
   const uint32_t max_lr = le < kMaxLr ? le : kMaxLr;
   const uint32_t P = (L + max_lr - 1) / max_lr;
@@ -606,6 +614,9 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     const bool prune = first && !last && ps.lr >= 4 &&
                        len_in <= ((n >> ps.lr) << (ps.lr - 3)) + (n >> ps.lr);
     const bool small = E <= kDSSmall;
+    // (round 3: an LDS floor of 54 / 80 KB per workgroup, i.e. 2 - 3 resident workgroups per
+    // CU so that a lone transform's tiles run in staggered generations, measured 3 - 7 %
+    // slower at 2^20 and 2^23: the lost occupancy costs more than the overlap gains)
     const size_t lds = ((size_t)(small ? kDSSmall : kDS) + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
                        kL * sizeof(uint32_t);
     dim3 grid(blocks, count);

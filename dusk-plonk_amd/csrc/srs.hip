@@ -156,7 +156,10 @@ int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   PLK_HIP_TRY(hipGetLastError());
   PLK_HIP_TRY(stream_wait(stream));
   s->ws.reset(new MsmWorkspace());
-  return ws_reserve(s, *s->ws, n, 1);
+  const int r = ws_reserve(s, *s->ws, n, 1, stream);
+  if (r != PLK_OK) return r;
+  PLK_HIP_TRY(stream_wait(stream));
+  return PLK_OK;
 }
 
 int srs_generate(plk_srs* s, const Fr& tau_mont, uint64_t start, hipStream_t stream) {

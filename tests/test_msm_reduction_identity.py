@@ -19,7 +19,7 @@ def weighted(S):
     return sum((b + 1) * s for b, s in enumerate(S))
 
 
-@pytest.mark.parametrize("K,nruns", [(16, 8), (16, 33), (4, 5)])
+@pytest.mark.parametrize("K,nruns", [(16, 8), (16, 33), (8, 9), (4, 5), (2, 17)])
 def test_run_sum_identity(K, nruns):
     rng = random.Random(K * 1000 + nruns)
     S = [rng.randrange(-10**6, 10**6) if rng.random() > 0.1 else 0 for _ in range(K * nruns)]
