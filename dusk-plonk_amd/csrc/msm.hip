@@ -126,9 +126,17 @@ __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cf
 
 // Per bucket, over the histogram workgroups: blockhist becomes the exclusive running count
 // (each workgroup's first position inside the bucket) and counts[b] the bucket total.
+// Workgroup (0, slot) also clears the slot's kChunkMax-word counters zero_a / zero_b when
+// given (the wide path's tail-length counters, used by k_fine and k_make_tasks_wide) — two
+// memset dispatches fewer per batch.
 __global__ void k_block_scan(uint32_t* __restrict__ blockhist, uint32_t nblk, uint32_t B,
-                             uint32_t* __restrict__ counts) {
+                             uint32_t* __restrict__ counts, uint32_t* __restrict__ zero_a,
+                             uint32_t* __restrict__ zero_b) {
   const uint32_t slot = blockIdx.y;
+  if (blockIdx.x == 0 && zero_a && threadIdx.x < kChunkMax) {
+    zero_a[(size_t)slot * kChunkMax + threadIdx.x] = 0;
+    zero_b[(size_t)slot * kChunkMax + threadIdx.x] = 0;
+  }
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   uint32_t* h = blockhist + (size_t)slot * nblk * B + b;
@@ -1016,8 +1024,6 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        batch, hdr_dev->flag, gen);
   }
   if (wide) {
-    PLK_HIP_TRY(hipMemsetAsync(w.len_cur.ptr, 0, (size_t)slots * kChunkMax * 4, stream));
-    PLK_HIP_TRY(hipMemsetAsync(w.len_fill.ptr, 0, (size_t)slots * kChunkMax * 4, stream));
     if (max_len) {
       hipLaunchKernelGGL(k_chist, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
                          cfg, NC, w.blockhist.as<uint32_t>());
@@ -1025,7 +1031,8 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
       PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * NC * 4, stream));
     }
     hipLaunchKernelGGL(k_block_scan, dim3(cdiv(NC, 256), slots), dim3(256), 0, stream,
-                       w.blockhist.as<uint32_t>(), hist_blocks, NC, w.counts.as<uint32_t>());
+                       w.blockhist.as<uint32_t>(), hist_blocks, NC, w.counts.as<uint32_t>(),
+                       w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>());
     hipLaunchKernelGGL(k_cscatter, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
                        cfg, NC, (uint64_t)s->n, (const uint32_t*)w.counts.as<uint32_t>(),
                        (const uint32_t*)w.blockhist.as<uint32_t>(), w.coarse_off.as<uint32_t>(),
@@ -1052,7 +1059,8 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
       PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * B * 4, stream));
     }
     hipLaunchKernelGGL(k_block_scan, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
-                       w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>());
+                       w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>(),
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
     hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
                        w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
                        w.task_off.as<uint32_t>(), w.full_off.as<uint32_t>(),

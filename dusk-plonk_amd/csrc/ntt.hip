@@ -477,11 +477,15 @@ static void plan_domain(plk_domain* d) {
   d->plan.clear();
   if (L == 0) return;
   // elements per workgroup: keep >= ~256 workgroups when the transform allows it, and at
-  // least 2^PLK_NTT_LE_MIN (experiments; default 2^6)
+  // least 2^10 (round 3; PLK_NTT_LE_MIN overrides for experiments). Small transforms (the
+  // 2^12..2^16 proofs' 2^12..2^17 ones) then take 1 024-element tiles of >= 4 columns
+  // (128-byte runs) instead of 64..256-element tiles of 1..2 columns: fewer, fuller
+  // workgroups and no 32-byte strided reads; 2^12 proofs 5.7 -> 6.3 M constraints/s, 2^16
+  // 23.4 -> 24.1 M (round 3 sweep, tools/gpu_r03_i.sh; 2^6 / 2^8 / 2^9 / 2^10 tried)
   static const uint32_t le_min = [] {
     const char* e = getenv("PLK_NTT_LE_MIN");
-    const int v = e ? atoi(e) : 6;
-    return (uint32_t)(v >= 1 && v <= (int)kMaxLe ? v : 6);
+    const int v = e ? atoi(e) : 10;
+    return (uint32_t)(v >= 1 && v <= (int)kMaxLe ? v : 10);
   }();
   uint32_t le = L > 8 ? L - 8 : 1;
   if (le < le_min) le = L < le_min ? L : le_min;

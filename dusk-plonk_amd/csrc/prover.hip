@@ -1024,7 +1024,6 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     TRY(P->evq.alloc(6 * nq * sizeof(Fr)));
     TRY(P->quotq.alloc(nq * sizeof(Fr)));
     TRY(P->t_coef.alloc(nq * sizeof(Fr)));
-    TRY(P->r_coef.alloc(S * sizeof(Fr)));
     TRY(P->agg.alloc(5 * n * sizeof(Fr)));
     TRY(P->agg2.alloc(S * sizeof(Fr)));
     TRY(P->w_coef.alloc((5 * n + S) * sizeof(Fr)));
@@ -1072,14 +1071,16 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     Fr* wl = P->wires_lag.as<Fr>();
     Fr* wc = P->wires_coef.as<Fr>();
     TRY(pk_gather_wires(P->witness.as<Fr>(), key->wire_idx.as<uint32_t>(), m, n, wl, s));
+    BlindBatch bb{};
+    bb.npoly = 4;
     for (int c = 0; c < 4; ++c) {
       TRY(ntt_run(key->dom, wl + c * n, wc + c * S, n, -1, 0, nsc, s, 1));
-      BlindArgs b{};
-      b.count = 2;
-      b.r[0] = rng.fr();
-      b.r[1] = rng.fr();
-      TRY(pk_blind(wc + c * S, n, b, s));
+      bb.poly[c] = wc + c * S;  // blind(1): b(X)(X^n - 1), two scalars per wire, drawn in order
+      bb.b[c].count = 2;
+      bb.b[c].r[0] = rng.fr();
+      bb.b[c].r[1] = rng.fr();
     }
+    TRY(pk_blind_batch(bb, n, s));
     plk_g1 wcom[4];
     TRY(prover_commit(P, {wc, wc + S, wc + 2 * S, wc + 3 * S}, {n + 2, n + 2, n + 2, n + 2}, wcom,
                       nullptr));
@@ -1121,14 +1122,28 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     const Fr fixed_sep = tr.challenge_scalar("fixed base separation challenge");
     const Fr var_sep = tr.challenge_scalar("variable base separation challenge");
     Fr* pil = P->pi_lag.as<Fr>();
-    if (!pis.empty()) PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
-    // pin_small: [0, #pi) PI values uploaded here, [#pi, #pi + 16) the evaluations read
-    // back in round 4 (sized once: queued copies keep pointing into it)
-    TRY(P->pin_small.alloc((pis.size() + 16) * sizeof(Fr)));
-    for (size_t i = 0; i < pis.size(); ++i) {
-      P->pin_small.as<Fr>()[i] = pis[i].second;
-      PLK_HIP_TRY(hipMemcpyAsync(pil + pis[i].first, P->pin_small.as<Fr>() + i, sizeof(Fr),
-                                 hipMemcpyHostToDevice, s));
+    // pin_small: [0, #pi) PI values uploaded here, [#pi, #pi + kMaxEval) the evaluations
+    // read back in round 4 (sized once: queued copies keep pointing into it)
+    TRY(P->pin_small.alloc((pis.size() + kMaxEval) * sizeof(Fr)));
+    // PI(X) = idft of the public-input vector (prover.rs:229): for a few public inputs
+    // straight from its definition, one product per input and coefficient (no upload, no
+    // transform); otherwise the vector is uploaded and transformed
+    const bool pi_direct = !pis.empty() && pis.size() <= (size_t)kPiDirect;
+    if (pi_direct) {
+      PiDirect pd{};
+      pd.count = (uint32_t)pis.size();
+      for (size_t i = 0; i < pis.size(); ++i) {
+        pd.idx[i] = pis[i].first;
+        pd.c[i] = fe_mul(pis[i].second, key->dom->n_inv);
+      }
+      TRY(pk_pi_coef(pd, key->dom->tw_inv.as<Fr>(), n, P->pi_coef.as<Fr>(), s));
+    } else if (!pis.empty()) {
+      PLK_HIP_TRY(hipMemsetAsync(pil, 0, n * sizeof(Fr), s));
+      for (size_t i = 0; i < pis.size(); ++i) {
+        P->pin_small.as<Fr>()[i] = pis[i].second;
+        PLK_HIP_TRY(hipMemcpyAsync(pil + pis[i].first, P->pin_small.as<Fr>() + i, sizeof(Fr),
+                                   hipMemcpyHostToDevice, s));
+      }
     }
     // the six polynomials over the quotient domain (quotient_poly.rs:54-58,145 over g H_8n
     // there): each a batch of the three coset blocks (prover.hpp) in one launch per pass
@@ -1141,7 +1156,8 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
       b.pre_stride = n + 8;
       return ntt_run_batch(key->domq, in, out, len, 1, 1, nsc, s, kQBlocks, b);
     };
-    if (!pis.empty()) TRY(ntt_run(key->dom, pil, P->pi_coef.as<Fr>(), n, -1, 0, nsc, s, 1));
+    if (!pis.empty() && !pi_direct)
+      TRY(ntt_run(key->dom, pil, P->pi_coef.as<Fr>(), n, -1, 0, nsc, s, 1));
     TRY(coset_fwd(zc, ev + 0 * nq, n + 3, key->coset_s));
     // wire evaluations at exponent -1 and PI at +1 for k_quotient's redundant-form
     // arithmetic (QuotientArgs): scaled coset tables, no extra pass
@@ -1248,41 +1264,69 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     const Fr zw = fe_mul(zeta, key->dom->omega);
     const Fr* qc = key->q_coef.as<Fr>();
     const Fr* sc = key->sigma_coef.as<Fr>();
+    // r(X) = sum_t s_t p_t(X) (arithmetic / range / logic / curve widgets' linearize and the
+    // permutation's): its polynomials p_t are known now, its scalars s_t only from the
+    // evaluations. So r is never formed: its terms' values at z join the batch of the 16
+    // proof evaluations (one launch, one read-back), r(z) = sum_t s_t p_t(z) is taken on the
+    // host — the same field element — and the opening aggregate carries v s_t p_t itself.
+    struct RTerm {
+      const Fr* p;
+      uint64_t len;
+      int ev;  // index of p(z) in the evaluation batch
+    };
+    std::vector<RTerm> rt;
     EvalBatch eb{};
     const Fr* polys[16] = {tc, wc, wc + S, wc + 2 * S, wc + 3 * S, sc, sc + n, sc + 2 * n,
                            qc + QARITH * n, qc + QC * n, qc + QL * n, qc + QR * n,
                            wc, wc + S, wc + 3 * S, zc};
     const uint64_t lens[16] = {3 * n + t4_len, n + 2, n + 2, n + 2, n + 2, n, n, n, n, n, n, n,
                                n + 2, n + 2, n + 2, n + 3};
-    for (int i = 0; i < 16; ++i) {
+    uint32_t ne = 0;
+    for (int i = 0; i < 16; ++i, ++ne) {
       eb.poly[i] = polys[i];
       eb.len[i] = lens[i];
       eb.x[i] = i < 12 ? zeta : zw;
     }
-    TRY(pk_eval(eb, 16, 3 * n + t4_len, P->eval_partial.as<Fr>(), P->eval_out.as<Fr>(), s));
-    Fr evs[16];
+    auto rterm = [&](const Fr* p, uint64_t len, int have) {
+      if (have < 0) {  // a new evaluation at z
+        eb.poly[ne] = p;
+        eb.len[ne] = len;
+        eb.x[ne] = zeta;
+        have = (int)ne++;
+      }
+      rt.push_back(RTerm{p, len, have});
+    };
+    // in the order the scalars are formed below
+    rterm(qc + QM * n, n, -1);
+    rterm(qc + QL * n, n, 10);
+    rterm(qc + QR * n, n, 11);
+    rterm(qc + QO * n, n, -1);
+    rterm(qc + Q4 * n, n, -1);
+    rterm(qc + QC * n, n, 9);
+    if (key->has_range) rterm(qc + QRANGE * n, n, -1);
+    if (key->has_logic) rterm(qc + QLOGIC * n, n, -1);
+    if (key->has_fixed) rterm(qc + QFIXED * n, n, -1);
+    if (key->has_var) rterm(qc + QVAR * n, n, -1);
+    rterm(zc, n + 3, -1);
+    rterm(sc + 3 * n, n, -1);
+    TRY(pk_eval(eb, ne, 3 * n + t4_len, P->eval_partial.as<Fr>(), P->eval_out.as<Fr>(), s));
+    Fr evs[kMaxEval];
     Fr* evs_pin = P->pin_small.as<Fr>() + pis.size();
-    PLK_HIP_TRY(hipMemcpyAsync(evs_pin, P->eval_out.ptr, sizeof evs, hipMemcpyDeviceToHost, s));
+    PLK_HIP_TRY(hipMemcpyAsync(evs_pin, P->eval_out.ptr, ne * sizeof(Fr), hipMemcpyDeviceToHost, s));
     PLK_HIP_TRY(stream_wait(s));
-    std::memcpy(evs, evs_pin, sizeof evs);
+    std::memcpy(evs, evs_pin, ne * sizeof(Fr));
     const Fr t_eval = evs[0], a_e = evs[1], b_e = evs[2], c_e = evs[3], d_e = evs[4];
     const Fr s1_e = evs[5], s2_e = evs[6], s3_e = evs[7];
     const Fr qar_e = evs[8], qc_e = evs[9], ql_e = evs[10], qr_e = evs[11];
     const Fr an_e = evs[12], bn_e = evs[13], dn_e = evs[14], perm_e = evs[15];
-    // r(X) = arithmetic::linearize + range::linearize + permutation::linearize
-    LinComb lc{};
-    auto term = [&](const Fr* p, uint64_t len, const Fr& sc_) {
-      lc.p[lc.terms] = p;
-      lc.len[lc.terms] = len;
-      lc.s[lc.terms] = sc_;
-      ++lc.terms;
-    };
-    term(qc + QM * n, n, fe_mul(qar_e, fe_mul(a_e, b_e)));
-    term(qc + QL * n, n, fe_mul(qar_e, a_e));
-    term(qc + QR * n, n, fe_mul(qar_e, b_e));
-    term(qc + QO * n, n, fe_mul(qar_e, c_e));
-    term(qc + Q4 * n, n, fe_mul(qar_e, d_e));
-    term(qc + QC * n, n, qar_e);
+    // the scalars s_t of r(X) = arithmetic::linearize + range::linearize + ... + permutation
+    std::vector<Fr> rs;
+    rs.push_back(fe_mul(qar_e, fe_mul(a_e, b_e)));  // q_m
+    rs.push_back(fe_mul(qar_e, a_e));               // q_l
+    rs.push_back(fe_mul(qar_e, b_e));               // q_r
+    rs.push_back(fe_mul(qar_e, c_e));               // q_o
+    rs.push_back(fe_mul(qar_e, d_e));               // q_4
+    rs.push_back(qar_e);                            // q_c
     if (key->has_range) {
       const Fr two = fe_dbl(one), three = fe_add(two, one);
       auto delta = [&](const Fr& f) {
@@ -1293,7 +1337,7 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
       r = fe_add(r, fe_mul(delta(fe_sub(b_e, four(c_e))), qa.kappa));
       r = fe_add(r, fe_mul(delta(fe_sub(a_e, four(b_e))), qa.kappa2));
       r = fe_add(r, fe_mul(delta(fe_sub(dn_e, four(a_e))), qa.kappa3));
-      term(qc + QRANGE * n, n, fe_mul(r, range_sep));
+      rs.push_back(fe_mul(r, range_sep));
     }
     if (key->has_logic) {  // logic::linearize: q_logic(X) * sep * (...) at the evaluations
       const Fr two = fe_dbl(one), three = fe_add(two, one), four = fe_dbl(two);
@@ -1308,17 +1352,17 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
       r = fe_add(r, fe_mul(delta(qd_), qa.lk2));
       r = fe_add(r, fe_mul(fe_sub(c_e, fe_mul(qa_, qb_)), qa.lk3));
       r = fe_add(r, fe_mul(logic_xor_and(qa_, qb_, c_e, qd_, qc_e), qa.lk4));
-      term(qc + QLOGIC * n, n, fe_mul(r, logic_sep));
+      rs.push_back(fe_mul(r, logic_sep));
     }
     if (key->has_fixed) {  // curve_scalar::linearize at the evaluations (q_l/q_r/q_c evals)
       const Fr w = widget_fixed_base(a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, ql_e, qr_e, qc_e,
                                      qa.fk, qa.fk2, qa.fk3, qa.edwards_d);
-      term(qc + QFIXED * n, n, fe_mul(w, fixed_sep));
+      rs.push_back(fe_mul(w, fixed_sep));
     }
     if (key->has_var) {  // curve_addtion::linearize
       const Fr w = widget_var_base(a_e, an_e, b_e, bn_e, c_e, d_e, dn_e, qa.vk, qa.vk2,
                                    qa.edwards_d);
-      term(qc + QVAR * n, n, fe_mul(w, var_sep));
+      rs.push_back(fe_mul(w, var_sep));
     }
     // z(X) * [(a + b z + g)(b + b K1 z + g)(c + b K2 z + g)(d + b K3 z + g) alpha + L1(z) alpha^2]
     const Fr bz = fe_mul(beta, zeta);
@@ -1328,21 +1372,16 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     idc = fe_mul(idc, alpha);
     const Fr zh = fe_sub(fe_pow_u64(zeta, n), one);  // Z_H(z)
     const Fr l1 = fe_mul(zh, fe_inv(fe_mul(fr_u64(n), fe_sub(zeta, one))));
-    term(zc, n + 3, fe_add(idc, fe_mul(l1, alpha2)));
+    rs.push_back(fe_add(idc, fe_mul(l1, alpha2)));
     // -sigma_4(X) * (a + b s1 + g)(b + b s2 + g)(c + b s3 + g) beta perm_eval alpha
     Fr cpc = fe_add(fe_add(a_e, fe_mul(beta, s1_e)), gamma);
     cpc = fe_mul(cpc, fe_add(fe_add(b_e, fe_mul(beta, s2_e)), gamma));
     cpc = fe_mul(cpc, fe_add(fe_add(c_e, fe_mul(beta, s3_e)), gamma));
     cpc = fe_mul(fe_mul(cpc, fe_mul(beta, perm_e)), alpha);
-    term(sc + 3 * n, n, fe_neg(cpc));
-    Fr* rc = P->r_coef.as<Fr>();
-    TRY(pk_lincomb(lc, rc, n + 3, s));
-    EvalBatch er{};
-    er.poly[0] = rc;
-    er.len[0] = n + 3;
-    er.x[0] = zeta;
-    TRY(pk_eval(er, 1, n + 3, P->eval_partial.as<Fr>(), P->eval_out.as<Fr>(), s));
-    const Fr r_e = d2h_fr(P->eval_out.as<Fr>(), s);
+    rs.push_back(fe_neg(cpc));
+    if (rs.size() != rt.size()) return PLK_E_DEVICE;  // the two lists are built in one order
+    Fr r_e = fe_zero<FrCfg>();  // r(z) = sum_t s_t p_t(z)
+    for (size_t t = 0; t < rt.size(); ++t) r_e = fe_add(r_e, fe_mul(rs[t], evs[rt[t].ev]));
 
     const char* elabels[17] = {"a_eval", "b_eval", "c_eval", "d_eval", "a_next_eval",
                                "b_next_eval", "d_next_eval", "s_sigma_1_eval", "s_sigma_2_eval",
@@ -1357,7 +1396,8 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     const Fr v2 = tr.challenge_scalar("v_challenge");
     const Fr zn = fe_pow_u64(zeta, n), z2n = fe_sqr(zn), z3n = fe_mul(z2n, zn);
     // W(X) = (sum v1^i p_i(X)) / (X - z), p = [quot, r, a, b, c, d, s1, s2, s3]
-    // with quot = t_low + z^n t_mid + z^2n t_high + z^3n t_4 expanded in place
+    // with quot = t_low + z^n t_mid + z^2n t_high + z^3n t_4 and r = sum_t s_t p_t expanded
+    // in place (scalars v1 s_t)
     LinComb la{};
     auto lt = [&](const Fr* p, uint64_t len, const Fr& sc_) {
       la.p[la.terms] = p;
@@ -1365,6 +1405,7 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
       la.s[la.terms] = sc_;
       ++la.terms;
     };
+    if (4 + rt.size() + 7 > (size_t)kMaxTerms) return PLK_E_DEVICE;
     // the aggregate and its quotient by (X - z) stop where t_4 does (same polynomials,
     // same commits)
     const uint64_t agg_len = std::max<uint64_t>(n + 3, t4_len);
@@ -1373,7 +1414,7 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     lt(tc + 2 * n, n, z2n);
     lt(tc + 3 * n, t4_len, z3n);
     Fr vp = v1;
-    lt(rc, n + 3, vp);
+    for (size_t t = 0; t < rt.size(); ++t) lt(rt[t].p, rt[t].len, fe_mul(vp, rs[t]));
     for (int c = 0; c < 4; ++c) {
       vp = fe_mul(vp, v1);
       lt(wc + c * S, n + 2, vp);

@@ -15,6 +15,19 @@ struct BlindArgs {
   Fr r[4];
   uint32_t count;
 };
+// PI(X) of a few public inputs straight from its definition (pk_pi_coef)
+constexpr int kPiDirect = 16;
+struct PiDirect {
+  uint64_t idx[kPiDirect];  // gate index of each public input
+  Fr c[kPiDirect];          // its value times n^-1 (R domain)
+  uint32_t count;
+};
+// the blinding of up to 4 polynomials in one launch (round 1's four wires)
+struct BlindBatch {
+  Fr* poly[4];
+  BlindArgs b[4];
+  uint32_t npoly;
+};
 
 // selector rows of the quotient-domain evaluation table
 enum { SEL_QM = 0, SEL_QL, SEL_QR, SEL_QO, SEL_Q4, SEL_QC, SEL_QARITH, SEL_QRANGE, SEL_QLOGIC,
@@ -57,14 +70,14 @@ struct QuotientArgs {
   Fr rx_inv32, rx_32;                   // 2^-5 and 2^5 (R domain): k_quotient_ext converts
 };
 
-constexpr int kMaxEval = 16;
+constexpr int kMaxEval = 28;  // 16 proof evaluations + the linearisation terms at z
 struct EvalBatch {
   const Fr* poly[kMaxEval];
   uint64_t len[kMaxEval];
   Fr x[kMaxEval];
 };
 
-constexpr int kMaxTerms = 12;
+constexpr int kMaxTerms = 24;  // the opening aggregate with r(X) expanded in place
 struct LinComb {
   const Fr* p[kMaxTerms];
   uint64_t len[kMaxTerms];
@@ -138,6 +151,10 @@ PLK_HD Fr widget_var_base(const Fr& x1, const Fr& x3, const Fr& y1, const Fr& y3
 int pk_gather_wires(const Fr* witness, const uint32_t* idx, uint64_t m, uint64_t n, Fr* out,
                     hipStream_t s);
 int pk_blind(Fr* poly, uint64_t n, const BlindArgs& b, hipStream_t s);
+int pk_blind_batch(const BlindBatch& bb, uint64_t n, hipStream_t s);
+// coefficients of PI(X) = idft(public-input vector) for at most kPiDirect public inputs:
+// out[j] = sum_k c_k w^(-idx_k j), w^-e from the domain's R'-domain table tw_inv
+int pk_pi_coef(const PiDirect& pd, const Fr* tw_inv, uint64_t n, Fr* out, hipStream_t s);
 int pk_fill(Fr* out, const Fr& v, uint64_t n, hipStream_t s);
 int pk_perm_numden(const Fr* wires, const Fr* sigmas, const Fr* elements, uint64_t n,
                    const Fr& beta, const Fr& gamma, const Fr& k1, const Fr& k2, const Fr& k3,
@@ -255,6 +272,6 @@ struct plk_prover {
   // per-proof scratch
   plk::PinnedBuf pin_witness, pin_small;  // host staging of the witness upload / small readbacks
   plk::DevBuf witness, wires_lag, wires_coef, z_lag, z_coef, num, den, tmp_a, scan_tmp, pi_lag,
-      pi_coef, evq, quotq, t_coef, r_coef, agg, agg2, w_coef, eval_partial, eval_out, ntt_scratch;
+      pi_coef, evq, quotq, t_coef, agg, agg2, w_coef, eval_partial, eval_out, ntt_scratch;
   ~plk_prover();
 };

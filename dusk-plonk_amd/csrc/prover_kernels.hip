@@ -81,6 +81,28 @@ __global__ void k_blind(Fr* __restrict__ poly, uint64_t n, BlindArgs b) {
   stf(&poly[n + i], b.r[i]);
 }
 
+// PI(X) = n^-1 sum_i v_i w^(-i j) summed over the few nonzero v_i: one product per public
+// input and coefficient instead of a transform (c_k = v_k n^-1 in the R domain times the
+// R'-domain table entry lands in the R domain)
+__global__ void k_pi_coef(PiDirect pd, const Fr* __restrict__ tw_inv, uint64_t n,
+                          Fr* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  RFr acc = rx_zero<FrCfg>();
+  for (uint32_t k = 0; k < pd.count; ++k)
+    acc = rx_add(acc, rx_mul(rx_unpack(pd.c[k]), ldr(&tw_inv[(pd.idx[k] * j) & (n - 1)])));
+  stf(&out[j], rx_pack_canonical(acc));
+}
+
+// thread 4p + i: coefficient i of polynomial p
+__global__ void k_blind_batch(BlindBatch bb, uint64_t n) {
+  const uint32_t p = threadIdx.x >> 2, i = threadIdx.x & 3;
+  if (p >= bb.npoly || i >= bb.b[p].count) return;
+  Fr* poly = bb.poly[p];
+  stf(&poly[i], fe_sub(ldf(&poly[i]), bb.b[p].r[i]));
+  stf(&poly[n + i], bb.b[p].r[i]);
+}
+
 __global__ void k_fill(Fr* __restrict__ out, Fr v, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) stf(&out[i], v);
@@ -524,6 +546,19 @@ int pk_gather_wires(const Fr* witness, const uint32_t* idx, uint64_t m, uint64_t
 
 int pk_blind(Fr* poly, uint64_t n, const BlindArgs& b, hipStream_t s) {
   hipLaunchKernelGGL(k_blind, dim3(1), dim3(64), 0, s, poly, n, b);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_pi_coef(const PiDirect& pd, const Fr* tw_inv, uint64_t n, Fr* out, hipStream_t s) {
+  if (pd.count > (uint32_t)kPiDirect || (n & (n - 1))) return PLK_E_ARG;
+  hipLaunchKernelGGL(k_pi_coef, dim3(blocks_for(n, 256)), dim3(256), 0, s, pd, tw_inv, n, out);
+  PLK_HIP_TRY(hipGetLastError());
+  return PLK_OK;
+}
+
+int pk_blind_batch(const BlindBatch& bb, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_blind_batch, dim3(1), dim3(64), 0, s, bb, n);
   PLK_HIP_TRY(hipGetLastError());
   return PLK_OK;
 }
