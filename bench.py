@@ -95,10 +95,9 @@ def parse():
                          "share per GPU), else every core in this process's affinity mask")
     ap.add_argument("--lanes", type=int, default=0,
                     help="concurrent prover lanes per GPU (prove mode): independent contexts "
-                         "with their own streams, each driven by a host thread. 0 = 8 at "
-                         "n >= 2^18, 12 at 2^15..2^17, 16 below (2 HIP hardware queues per "
-                         "lane; tools/gpu_lanes_small.sh: 2^16 20.7/21.0/22.0/21.1 M and "
-                         "2^12 3.25/3.60/3.78/3.82 M constraints/s at 10/12/14/16 lanes)")
+                         "with their own streams, each driven by a host thread. 0 = 12 at "
+                         "n >= 2^18, 14 at 2^15..2^17, 16 below (2 HIP hardware queues per "
+                         "lane; round-3 sweep tools/gpu_r03_lanes.sh in DESIGN §6)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4); "
                          "0 = min(32, 2 x lanes): more lanes than queues serialise on them")
@@ -854,8 +853,11 @@ def main():
         raise SystemExit(launch_ranks(args.gpus))
     if world_env is not None and args.gpus is not None and args.gpus != int(world_env):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
-    if args.lanes <= 0:  # tools/gpu_lanes_small.sh: 2^12 3.6 -> 3.9 M at 12 -> 16 lanes
-        args.lanes = 8 if args.log_n >= 18 else 12 if args.log_n >= 15 else 16
+    if args.lanes <= 0:
+        # round-3 sweep (tools/gpu_r03_lanes.sh): 2^20 30.2 / 30.3 / 30.7 / 31.4 M at 6 / 8 /
+        # 10 / 12 lanes; 2^16 24.0 / 24.6 / 25.1 / 22.0 M at 10 / 12 / 14 / 16; 2^12 5.4 / 5.9
+        # M at 12 / 16
+        args.lanes = 12 if args.log_n >= 18 else 14 if args.log_n >= 15 else 16
     if args.mode == "prove":
         # before the HIP runtime starts (the torch import below): each lane's stream gets a
         # hardware queue of its own

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "internal.hpp"
@@ -317,15 +318,26 @@ constexpr uint32_t kCoarseMax = 4096;        // coarse bins (B <= 2^22, c <= 23)
 // bucket reduction: runs of K = 2^rb buckets per lane. Batches of several MSMs (the
 // prover's commit groups, with other proofs' kernels beside them) take 16. A lone MSM's
 // run-sum chains are latency-bound with the chip otherwise idle, so its rb is the largest
-// rb <= kRunBits that still gives kRunLanes run lanes: 4 at 2^20 (round 2: a fixed 8), 2 at
-// 2^16 (lone 2^16 MSM 1.14 -> 1.01 ms). Applied to batches too it cost the 2^16 proof
+// rb <= kRunBits that still gives kRunLanes run lanes: K = 8 at 2^20, 2 at 2^16 (lone
+// 2^16 MSM 1.14 -> 1.01 ms in round 2). Applied to batches too it cost the 2^16 proof
 // 22 -> 18 M constraints/s (more bit-sum groups, NR / 256, in every commit group).
 constexpr uint32_t kRunBits = 4, kRunBitsMin = 1;
-constexpr size_t kRunLanes = 131072;  // two waves per SIMD of the run-sum kernels
+// run lanes aimed at: 65536 (one wave per SIMD) — with the 4-lane k_bitsum1 a lone 2^20
+// MSM then runs rb = 3, 256 bit-sum groups: 3.44 -> 3.34 ms (131072: rb = 2, 512 groups)
+constexpr size_t kRunLanes = 65536;
+// kRunLanes, or PLK_RUN_LANES from the environment (sweeps)
+inline size_t run_lanes() {
+  static const size_t v = [] {
+    const char* e = getenv("PLK_RUN_LANES");
+    const long long x = e ? atoll(e) : 0;
+    return x > 0 ? (size_t)x : kRunLanes;
+  }();
+  return v;
+}
 inline uint32_t run_bits(uint32_t B, uint32_t slots) {
   if (slots > 1) return kRunBits;
   uint32_t rb = kRunBits;
-  while (rb > kRunBitsMin && (size_t)(B >> rb) < kRunLanes) --rb;
+  while (rb > kRunBitsMin && (size_t)(B >> rb) < run_lanes()) --rb;
   return rb;
 }
 
@@ -641,6 +653,42 @@ __device__ __forceinline__ RFp shfl_down_rfp(const RFp& v, uint32_t h) {
   return rx_unpack(x);
 }
 
+__device__ __forceinline__ G1R shfl_down_g1r(const G1R& v, uint32_t h) {
+  G1R o;
+  o.X = shfl_down_rfp(v.X, h);
+  o.Y = shfl_down_rfp(v.Y, h);
+  o.ZZ = shfl_down_rfp(v.ZZ, h);
+  o.ZZZ = shfl_down_rfp(v.ZZZ, h);
+  return o;
+}
+
+// Sum over groups of w consecutive lanes (w a power of two <= 64, groups aligned; e = lane
+// index in the group): lane e = 0 of each group ends with the group's sum. LAZY: g1r_add_lazy
+// (straight-line, exceptional cases repaired after; ~275 VGPRs) or the branching g1r_add
+// (~205 VGPRs: two waves per SIMD). One dependent addition costs a lone wave 12.5 / 14.3 us
+// (tools/ubench_tail.hip, profiles/r03_ubench_tail.txt).
+template <bool LAZY>
+__device__ __forceinline__ G1R g1r_add_t(const G1R& a, const G1R& b) {
+  return LAZY ? g1r_add_lazy(a, b) : g1r_add(a, b);
+}
+template <bool LAZY>
+__device__ __forceinline__ G1R shfl_tree(G1R acc, uint32_t e, uint32_t w) {
+  for (uint32_t h = w >> 1; h >= 1; h >>= 1) {
+    const G1R o = shfl_down_g1r(acc, h);
+    if (e < h) acc = g1r_add_t<LAZY>(acc, o);
+  }
+  return acc;
+}
+
+// k_bitsum1: the branching addition at two waves per SIMD (2 workgroups of 256 per CU: a lone
+// 2^20 MSM's 512 groups in one round instead of two)
+#ifndef PLK_BITSUM_LAZY
+#define PLK_BITSUM_LAZY 0
+#endif
+#ifndef PLK_BITSUM_WAVES
+#define PLK_BITSUM_WAVES 2
+#endif
+
 __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__ task_off,
                                                     uint32_t B, uint32_t lp, uint64_t task_stride,
                                                     const G1xyzz* __restrict__ partials,
@@ -650,15 +698,12 @@ __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__
   const uint32_t b = (blockIdx.x * 256 + tid) >> lp;
   task_off += (size_t)slot * (B + 1);
   partials += (size_t)slot * task_stride;
+  // the branching g1r_add here: ~200 VGPRs (2 waves per SIMD) against ~325 for the lazy form
   G1R acc = g1r_infinity();
   if (b < B)
     for (uint32_t t = task_off[b] + s; t < task_off[b + 1]; t += P) acc = g1r_add(acc, ld_g1r(&partials[t]));
   for (uint32_t h = P >> 1; h >= 1; h >>= 1) {  // lanes s < h add lane s + h (same bucket)
-    G1R o;
-    o.X = shfl_down_rfp(acc.X, h);
-    o.Y = shfl_down_rfp(acc.Y, h);
-    o.ZZ = shfl_down_rfp(acc.ZZ, h);
-    o.ZZZ = shfl_down_rfp(acc.ZZZ, h);
+    const G1R o = shfl_down_g1r(acc, h);
     if (s < h) acc = g1r_add(acc, o);
   }
   if (s == 0 && b < B) st_g1r(&bsum[(size_t)slot * B + b], acc);
@@ -738,7 +783,7 @@ __global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, u
 // j < 4 is a sum of the 8 columns with bit j of c set and T_(4+i) a sum of the 8 rows with
 // bit i of a set; A_g is the sum of the rows: 480 + 71 additions per 256 buckets instead of
 // the 1 144 of bit sums taken over the buckets themselves.
-// k_bitsum1 (one workgroup of 256 lanes per g): the bucket sums S (k_bucket_sum), the 32
+// k_bitsum1 (one workgroup per g): the bucket sums S (k_bucket_sum), the 32
 // row / column sums (8 consecutive lanes each: one addition, then a 3-level shuffle tree),
 // then the 9 outputs from them (wave 0). out[slot][g][0..7] = T_j(g), [8] = A_g; with `zin`
 // (wide bucket sets) also [9] = the plain sum of the group's 256 Z values (k_runsum).
@@ -750,13 +795,19 @@ __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
 }
 
 template <bool Z>
-__global__ void __launch_bounds__(Z ? 384 : 256) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
-                                                           const G1xyzz* __restrict__ zin,
-                                                           G1xyzz* __restrict__ out) {
+__global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
+                                                                           const G1xyzz* __restrict__ zin,
+                                                                           G1xyzz* __restrict__ out) {
   // the group's values (buckets or run sums Y; with Z also the 256 plain-sum values) are
   // read straight from HBM and the trees run over cross-lane shuffles: LDS holds only the
   // NS row / column sums (9 KiB instead of 105 — a resident k_bitsum1 used to keep the other
-  // proofs' NTT passes off its CU)
+  // proofs' NTT passes off its CU).
+  // The NS sums of 16 take 4 consecutive lanes each, and each lane first adds its 4 members
+  // in sequence (every lane busy), then a 2-level shuffle tree: 3 + 2 levels on NS / 16 waves.
+  // The tree kernels are issue-bound — a wave issues the whole addition however few of its
+  // lanes are active — so lanes idle in a shuffle level cost as much as busy ones: 8 lanes
+  // per sum with 2 members each (3-level tree) issued twice the wave-additions (round 3:
+  // 8 waves x 4 levels + 4 against 3 waves x 5 levels + 4 per group).
   constexpr uint32_t NS = Z ? 48 : 32;
   __shared__ G1xyzz sh[NS];
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
@@ -766,27 +817,20 @@ __global__ void __launch_bounds__(Z ? 384 : 256) k_bitsum1(uint32_t B, const G1x
     const G1xyzz* src = x < 256 ? bsum : zin;
     return b < B ? ld_g1r(&src[(size_t)slot * B + b]) : g1r_infinity();
   };
-  auto shfl_down_g1r = [](const G1R& v, uint32_t h) {
-    G1R o;
-    o.X = shfl_down_rfp(v.X, h);
-    o.Y = shfl_down_rfp(v.Y, h);
-    o.ZZ = shfl_down_rfp(v.ZZ, h);
-    o.ZZZ = shfl_down_rfp(v.ZZZ, h);
-    return o;
-  };
-  {  // sum q < 16: row a = q; 16 <= q < 32: column c = q - 16; q >= 32 (Z): row q - 32 of the
-     // plain-sum values. Lane e of its 8 (consecutive lanes) adds members 2e, 2e + 1.
-    const uint32_t q = tid >> 3, e = tid & 7;
-    const uint32_t m0 = q < 16 ? 16 * q + 2 * e : q < 32 ? (q - 16) + 32 * e : 256 + 16 * (q - 32) + 2 * e;
-    const uint32_t m1 = (q >= 16 && q < 32) ? m0 + 16 : m0 + 1;
-    G1R acc = g1r_add(value(m0), value(m1));
-    for (uint32_t h = 4; h >= 1; h >>= 1) {
-      const G1R o = shfl_down_g1r(acc, h);
-      if (e < h) acc = g1r_add(acc, o);
-    }
+  {  // sum q < 16: row a = q (members 16q + c); 16 <= q < 32: column c = q - 16 (members
+     // c + 16a); q >= 32 (Z): row q - 32 of the plain-sum values. Lane e < 4 of the sum's 4
+     // takes members 4e .. 4e + 3 of its row / column.
+    const uint32_t q = tid >> 2, e = tid & 3;
+    auto member = [&](uint32_t i) {  // i-th member of sum q, i < 16
+      return q < 16 ? 16 * q + i : q < 32 ? (q - 16) + 16 * i : 256 + 16 * (q - 32) + i;
+    };
+    G1R acc = value(member(4 * e));
+#pragma unroll 1
+    for (uint32_t i = 1; i < 4; ++i) acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, value(member(4 * e + i)));
+    acc = shfl_tree<PLK_BITSUM_LAZY>(acc, e, 4);
     if (e == 0) st_g1r(&sh[q], acc);
-    __syncthreads();
   }
+  __syncthreads();
   // wave 0: lanes 0..31 = T_0..T_7, 4 lanes each (2 terms per lane); lanes 32..39 = A_g, 8 lanes
   // (rows 2e, 2e + 1); with Z lanes 40..47 = the plain sum (its rows 2e, 2e + 1); then trees
   if (tid < 64) {
@@ -804,10 +848,10 @@ __global__ void __launch_bounds__(Z ? 384 : 256) k_bitsum1(uint32_t B, const G1x
       i0 = (s == 8 ? 0 : 32) + 2 * e;
       i1 = i0 + 1;
     }
-    G1R acc = on ? g1r_add(ld_g1r(&sh[i0]), ld_g1r(&sh[i1])) : g1r_infinity();
+    G1R acc = on ? g1r_add_t<PLK_BITSUM_LAZY>(ld_g1r(&sh[i0]), ld_g1r(&sh[i1])) : g1r_infinity();
     for (uint32_t h = 4; h >= 1; h >>= 1) {  // groups of w consecutive lanes
       const G1R o = shfl_down_g1r(acc, h);
-      if (on && e < h && h < w) acc = g1r_add(acc, o);
+      if (on && e < h && h < w) acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, o);
     }
     if (on && e == 0) st_g1r(&out[s], acc);
   }
@@ -828,42 +872,39 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
   if (j == 0 && tid == 0) entries[slot] = offsets[(size_t)slot * (B + 1) + B];
   in += (size_t)slot * G * kBitsumOut;
+  // lazy additions (one wave per SIMD is all this narrow kernel runs); the stored totals are
+  // finished to [0, 2p) for the host. A lane's first term is taken as is (adding it to
+  // infinity would run the repair path).
   G1R acc = g1r_infinity();
+  bool have = false;
   for (uint32_t g = tid; g < G; g += 256) {
     const G1xyzz* e = &in[(size_t)g * kBitsumOut];
-    if (j >= nbits) {  // wide sets: sum_g of the plain sums (j = nbits) and of A_g (nbits + 1)
-      acc = g1r_add(acc, ld_g1r(&e[j == nbits ? 9 : 8]));
-    } else if (j < 8) {
-      acc = g1r_add(acc, ld_g1r(&e[j]));
-      if (j == 0) acc = g1r_add(acc, ld_g1r(&e[8]));
-    } else if ((g >> (j - 8)) & 1u) {
-      acc = g1r_add(acc, ld_g1r(&e[8]));
+    // wide sets: j = nbits sums the plain sums, nbits + 1 the A_g
+    uint32_t i0 = kBitsumOut, i1 = kBitsumOut;  // kBitsumOut: none
+    if (j >= nbits) i0 = j == nbits ? 9 : 8;
+    else if (j < 8) i0 = j, i1 = j == 0 ? 8 : kBitsumOut;
+    else if ((g >> (j - 8)) & 1u) i0 = 8;
+    for (uint32_t i : {i0, i1}) {
+      if (i == kBitsumOut) continue;
+      const G1R v = ld_g1r(&e[i]);
+      if (have) acc = g1r_add_lazy(acc, v);
+      else acc = v;
+      have = true;
     }
   }
   // lanes >= G hold infinity: a shuffle tree over each wave's min(G, 64) lanes, then the
   // wave totals through LDS (768 B instead of a 48 KiB tree)
-  for (uint32_t h = min(G, 64u) >> 1; h >= 1; h >>= 1) {
-    G1R o;
-    o.X = shfl_down_rfp(acc.X, h);
-    o.Y = shfl_down_rfp(acc.Y, h);
-    o.ZZ = shfl_down_rfp(acc.ZZ, h);
-    o.ZZZ = shfl_down_rfp(acc.ZZZ, h);
-    if ((tid & 63) < h) acc = g1r_add(acc, o);
-  }
+  acc = shfl_tree<true>(acc, tid & 63, min(G, 64u));
   const uint32_t nw = min(G, 256u) > 64 ? min(G, 256u) >> 6 : 1;  // waves holding values
   if ((tid & 63) == 0 && (tid >> 6) < nw) st_g1r(&sh[tid >> 6], acc);
   __syncthreads();
   if (tid < 2) {  // the (up to) 4 wave totals as a 2-level tree: lanes 0 / 1 add a pair each
     acc = 2 * tid < nw ? ld_g1r(&sh[2 * tid]) : g1r_infinity();
-    if (2 * tid + 1 < nw) acc = g1r_add(acc, ld_g1r(&sh[2 * tid + 1]));
+    if (2 * tid + 1 < nw) acc = g1r_add_lazy(acc, ld_g1r(&sh[2 * tid + 1]));
   }
   if (tid < 64) {  // wave 0 whole: the shuffle reads lane 1
-    G1R o;
-    o.X = shfl_down_rfp(acc.X, 1);
-    o.Y = shfl_down_rfp(acc.Y, 1);
-    o.ZZ = shfl_down_rfp(acc.ZZ, 1);
-    o.ZZZ = shfl_down_rfp(acc.ZZZ, 1);
-    if (tid == 0) st_g1r(&out[(size_t)slot * nout + j], nw > 2 ? g1r_add(acc, o) : acc);
+    const G1R o = shfl_down_g1r(acc, 1);
+    if (tid == 0) st_g1r(&out[(size_t)slot * nout + j], g1r_lazy_finish(nw > 2 ? g1r_add_lazy(acc, o) : acc));
   }
 }
 
@@ -910,7 +951,7 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
   const size_t NC = B >> kFineBits;
   // runs over all slots of a batch (run_bits: a batch runs B >> kRunBits per slot, a lone
   // MSM fewer than 2 kRunLanes unless rb = kRunBits)
-  const size_t max_runs = std::max<size_t>(slots * (B >> kRunBits), 2 * kRunLanes);
+  const size_t max_runs = std::max<size_t>(slots * (B >> kRunBits), B >> kRunBitsMin);
   if (wide && NC > kCoarseMax) return PLK_E_ARG;
   const size_t entries = (size_t)s->windows * len;
   const size_t max_tasks = entries / kChunkMin + B + 1;
@@ -999,12 +1040,14 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
   const uint32_t nout = nbits + (wide ? 2u : 0u);         // + sum_r T_r, sum_r Y_r
   const uint32_t slots = (uint32_t)count;
-  // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads; wide
-  // sets have few entries per bucket and enough tasks anyway: one task per bucket
-  const uint32_t chunk =
-      wide ? kChunkMax
-           : (uint32_t)std::min<size_t>(kChunkMax,
-                                        std::max<size_t>(kChunkMin, total_entries / PLK_CHUNK_TARGET));
+  // chunk so that the accumulation grid holds ~2 waves of the chip's resident threads. Wide
+  // sets in a batch have few entries per bucket and enough tasks anyway: one task per bucket.
+  // A lone wide MSM below ~2^18 points (configs[2]-style commits at 2^16) would leave one
+  // task of ~15-35 dependent additions per bucket on a half-empty chip: it takes the chunk
+  // formula too (16 at 2^16, 52 at 2^20)
+  const uint32_t chunk_fit =
+      (uint32_t)std::min<size_t>(kChunkMax, std::max<size_t>(kChunkMin, total_entries / PLK_CHUNK_TARGET));
+  const uint32_t chunk = wide && count > 1 ? kChunkMax : chunk_fit;
   const size_t max_tasks_used = (size_t)s->windows * max_len / chunk + B;
   // 256 workgroups per slot: fewer give longer per-bucket write runs in k_scatter but lose
   // more parallelism than they gain (measured 2.77 / 2.79 / 3.02 / 4.52 ms per proof at
@@ -1113,11 +1156,11 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
   }
   if (wide) {
-    hipLaunchKernelGGL(k_bitsum1<true>, dim3(G, slots), dim3(384), 0, stream, NR,
+    hipLaunchKernelGGL(k_bitsum1<true>, dim3(G, slots), dim3(192), 0, stream, NR,
                        (const G1xyzz*)w.ys.as<G1xyzz>(), (const G1xyzz*)w.zs.as<G1xyzz>(),
                        w.bits1.as<G1xyzz>());
   } else {
-    hipLaunchKernelGGL(k_bitsum1<false>, dim3(G, slots), dim3(256), 0, stream, B,
+    hipLaunchKernelGGL(k_bitsum1<false>, dim3(G, slots), dim3(128), 0, stream, B,
                        (const G1xyzz*)w.bsum.as<G1xyzz>(), (const G1xyzz*)nullptr,
                        w.bits1.as<G1xyzz>());
   }
