@@ -71,6 +71,10 @@ constexpr bool kFuseFirstStep = PLK_NTT_FUSE != 0;
 #ifndef PLK_NTT_MINW
 #define PLK_NTT_MINW 1
 #endif
+// the persistent variant's (PF): its prefetched loads stay live across the butterflies
+#ifndef PLK_NTT_PF_MINW
+#define PLK_NTT_PF_MINW 2
+#endif
 
 // Element idx of a data plane sits at word idx ^ ((idx / 32) * 9 mod 32): ds_read_b32 /
 // ds_write_b32 bank by word mod 32 per 32-lane half, and the unswizzled columns put the
@@ -243,8 +247,8 @@ __device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uin
 // with x_(j+R/8) = 0 except for j = 0 — the 8n coset transforms of the prover's
 // (n + small)-coefficient polynomials. They are computed directly from the loaded rows
 // (7 multiplies per row instead of three stages of butterflies over 8x the rows).
-template <int PRE, int POST, int PRUNE, uint32_t DS>
-__global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
+template <int PRE, int POST, int PRUNE, uint32_t DS, bool PF>
+__global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                   const Fr* __restrict__ tw,
                                                   const Fr* __restrict__ ptw,
                                                   const Fr* __restrict__ pre,
@@ -268,10 +272,50 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
 
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   const uint32_t nr_log = log_n - lr;  // log2(N/R)
-  const uint32_t i0 = blockIdx.x << lt;
 
   for (uint32_t x = tid; x < TS; x += bd) lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
   for (uint32_t x = tid; x < kQMax * kL; x += bd) ztab[x] = kZTab.v[x];
+
+  // every load of the thread's (at most kLoadIt, E / bd <= 4) elements is issued before the
+  // first multiply: one HBM latency per pass instead of one per element
+  // The loads are unconditional (clamped indices; the host passes a valid `in` even for
+  // len_in = 0) and zero-padding is a select afterwards: a conditional load would merge
+  // with its alternative at a join and wait there.
+  constexpr uint32_t kLoadIt = 4;
+  const uint32_t nit = (E + bd - 1) / bd;  // uniform, <= kLoadIt
+  Fr raw[kLoadIt], aux[kLoadIt];           // input; coset factor (PRE) or inter-pass twiddle
+  auto issue = [&](uint32_t i0) {          // the loads of the tile of columns i0 .. i0 + T - 1
+#pragma unroll
+    for (uint32_t c = 0; c < kLoadIt; ++c) {  // all kLoadIt (duplicates past E / bd)
+      const uint32_t e = min(tid + c * bd, E - 1);
+      const size_t g = (size_t)(i0 + (e & (T - 1))) + ((size_t)(e >> lt) << nr_log);
+      const size_t gc = g < len_in ? g : 0;
+      raw[c] = ld_fr(&in[gc]);
+      if (PRE == 1) aux[c] = ld_fr(&pre[gc]);
+    }
+    // inter-pass twiddle w_{Rp}^{jk} from the pass table laid out [j][k] (coalesced in k);
+    // every (j, k) is in the table, the j = 0 / k = 0 entries are skipped below
+    if (PRE != 1 && lp != 0) {
+#pragma unroll
+      for (uint32_t c = 0; c < kLoadIt; ++c) {
+        const uint32_t e = min(tid + c * bd, E - 1);
+        aux[c] = ld_fr(&ptw[((size_t)(e >> lt) << lp) + ((i0 + (e & (T - 1))) & (p - 1))]);
+      }
+    }
+  };
+  // PF (persistent, software-pipelined; opt-in, PLK_NTT_PF): the grid holds fewer workgroups
+  // than tiles and each takes tiles blockIdx.x, + gridDim.x, ...; the next tile's loads are
+  // issued as soon as the current tile's inputs sit in LDS, so they run under its
+  // butterflies and stores (a lone transform's tiles otherwise all load, compute and store in
+  // lockstep). Measured slower (round 3, tools/gpu_r03_pf*.sh, dft + idft per step): 2^20
+  // 0.305 ms off / 0.332 at 512 workgroups (2 waves per SIMD, 204 VGPRs) / 0.35 at 768 (3
+  // waves, 168 VGPRs + spills); 2^23 1.94 / 2.35 / 2.37 — the registers that carry the next
+  // tile's loads cost more occupancy than the overlap returns.
+  const uint32_t nblk = 1u << (log_n - lr - lt);
+  uint32_t tile = blockIdx.x;
+  if (PF) issue(tile << lt);
+  for (;;) {
+  const uint32_t i0 = tile << lt;
 
   // radix-2 stages left: the first radix-4 step's half is 2^(lh-1) (three stages done in
   // closed form when pruning)
@@ -308,31 +352,7 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
     }
   }
   if (!PRUNE) {
-    // every load of the thread's (at most kLoadIt, E / bd <= 4) elements is issued before the
-    // first multiply: one HBM latency per pass instead of one per element
-    // The loads are unconditional (clamped indices; the host passes a valid `in` even for
-    // len_in = 0) and zero-padding is a select afterwards: a conditional load would merge
-    // with its alternative at a join and wait there.
-    constexpr uint32_t kLoadIt = 4;
-    const uint32_t nit = (E + bd - 1) / bd;  // uniform, <= kLoadIt
-    Fr raw[kLoadIt], aux[kLoadIt];           // input; coset factor (PRE) or inter-pass twiddle
-#pragma unroll
-    for (uint32_t c = 0; c < kLoadIt; ++c) {  // all kLoadIt (duplicates past E / bd)
-      const uint32_t e = min(tid + c * bd, E - 1);
-      const size_t g = (size_t)(i0 + (e & (T - 1))) + ((size_t)(e >> lt) << nr_log);
-      const size_t gc = g < len_in ? g : 0;
-      raw[c] = ld_fr(&in[gc]);
-      if (PRE == 1) aux[c] = ld_fr(&pre[gc]);
-    }
-    // inter-pass twiddle w_{Rp}^{jk} from the pass table laid out [j][k] (coalesced in k);
-    // every (j, k) is in the table, the j = 0 / k = 0 entries are skipped below
-    if (PRE != 1 && lp != 0) {
-#pragma unroll
-      for (uint32_t c = 0; c < kLoadIt; ++c) {
-        const uint32_t e = min(tid + c * bd, E - 1);
-        aux[c] = ld_fr(&ptw[((size_t)(e >> lt) << lp) + ((i0 + (e & (T - 1))) & (p - 1))]);
-      }
-    }
+    if (!PF) issue(i0);
     auto input = [&](uint32_t c) -> RFr {  // element tid + c bd, pre-scaled / twiddled
       const uint32_t e = tid + c * bd;
       const uint32_t t = e & (T - 1), j = e >> lt;
@@ -365,6 +385,7 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
         if (e < E) lds_std<DS>(data, ((e >> lt) << lt) + (e & (T - 1)), v);
       }
     }
+    if (PF && tile + gridDim.x < nblk) issue((tile + gridDim.x) << lt);  // next tile's loads
   }
   __syncthreads();
 
@@ -417,6 +438,11 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
     else if (POST == 2) v = rx_mul(v, ld_rfr(&post[pos]));
     else v = reduce_q(v, ztab);  // < 1.6r
     st_fr(&out[pos], rx_pack_canonical(v));
+  }
+  if (!PF) break;
+  tile += gridDim.x;
+  if (tile >= nblk) break;
+  __syncthreads();  // the output reads of this tile before the next tile's LDS stores
   }
 }
 
@@ -623,7 +649,14 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     // slower at 2^20 and 2^23: the lost occupancy costs more than the overlap gains)
     const size_t lds = ((size_t)(small ? kDSSmall : kDS) + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
                        kL * sizeof(uint32_t);
-    dim3 grid(blocks, count);
+    // persistent software-pipelined passes (k_ntt_pass PF): a lone large transform's grid of
+    // pf_grid workgroups, each taking blocks / pf_grid tiles (PLK_NTT_PF = the grid size, 0 off)
+    static const uint32_t pf_grid = [] {
+      const char* e = getenv("PLK_NTT_PF");
+      return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    const bool pf = pf_grid > 0 && !prune && !small && count == 1 && blocks > pf_grid;
+    dim3 grid(pf ? pf_grid : blocks, count);
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
     NttStrides str;
@@ -631,15 +664,16 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     str.out = last ? bt.out_stride : n * 1;
     str.pre = bt.pre ? bt.pre_stride : 0;
     str.post = bt.post ? bt.post_stride : 0;
-#define PLK_LAUNCH_DS(PRE, POST, PRUNE, DS)                                               \
-  hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE, DS>), grid, dim3(bd), lds, stream, src, dst, tw, \
+#define PLK_LAUNCH_DS(PRE, POST, PRUNE, DS, PF)                                           \
+  hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE, DS, PF>), grid, dim3(bd), lds, stream, src, dst, tw, \
                      ptw, pre_table ? pre_table : d->coset_pow.as<Fr>(),               \
                      bt.post ? bt.post : d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n, \
                      ps.lp, ps.lr, ps.lt, lin, str)
-#define PLK_LAUNCH(PRE, POST, PRUNE)                    \
-  do {                                                  \
-    if (small) PLK_LAUNCH_DS(PRE, POST, PRUNE, kDSSmall); \
-    else PLK_LAUNCH_DS(PRE, POST, PRUNE, kDS);          \
+#define PLK_LAUNCH(PRE, POST, PRUNE)                              \
+  do {                                                            \
+    if (small) PLK_LAUNCH_DS(PRE, POST, PRUNE, kDSSmall, false);   \
+    else if (!PRUNE && pf) PLK_LAUNCH_DS(PRE, POST, 0, kDS, true); \
+    else PLK_LAUNCH_DS(PRE, POST, PRUNE, kDS, false);             \
   } while (0)
     if (prune) {
       if (pre == 1) PLK_LAUNCH(1, 0, 1);

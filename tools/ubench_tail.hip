@@ -42,6 +42,67 @@ __global__ void __launch_bounds__(256, W) k_chain(const G1xyzz* __restrict__ in,
   st_g1r(&out[t], acc);
 }
 
+// ---- experiment: one lazy full addition on the 4 lanes of a quad ----------------------
+// Lanes 4i .. 4i + 3 hold the same operands and end with the same result; each round every
+// lane forms ONE of the independent products of g1r_add_lazy_sl (operands picked per lane)
+// and the results are broadcast through DPP quad permutations: 4 rounds (the 4th a fused
+// product pair) instead of 13 products. Bit-identical to g1r_add_lazy, but a lone wave
+// gains only 12.4 -> 9.8 us per dependent addition: one product alone in a round is
+// latency-bound (~2.4 us, ~3x its issue cost), and the serial formula's critical path is
+// itself ~5 dependent products. Kept here, not in the product (round-3 DESIGN §3).
+template <int K>
+__device__ __forceinline__ RFp rx_quad_bcast(const RFp& v) {  // lane K of the quad, to all 4
+  constexpr int kCtrl = K | (K << 2) | (K << 4) | (K << 6);       // quad_perm [K, K, K, K]
+  RFp r;
+#pragma unroll
+  for (int i = 0; i < RxShape<FpCfg>::L; ++i)
+    r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], kCtrl, 0xF, 0xF, false);
+  return r;
+}
+
+__device__ __forceinline__ RFp rx_sel4(uint32_t k, const RFp& a0, const RFp& a1, const RFp& a2,
+                                       const RFp& a3) {
+  RFp r;
+#pragma unroll
+  for (int i = 0; i < RxShape<FpCfg>::L; ++i)
+    r.v[i] = k == 0 ? a0.v[i] : k == 1 ? a1.v[i] : k == 2 ? a2.v[i] : a3.v[i];
+  return r;
+}
+
+__device__ __forceinline__ G1R g1r_add_lazy_quad(const G1R& p, const G1R& q) {
+  const uint32_t k = __lane_id() & 3;
+  // round 1: U1 = X1 ZZ2, U2 = X2 ZZ1, S1 = Y1 ZZZ2, S2 = Y2 ZZZ1
+  const RFp m1 = rx_mul(rx_sel4(k, p.X, q.X, p.Y, q.Y), rx_sel4(k, q.ZZ, p.ZZ, q.ZZZ, p.ZZZ));
+  const RFp U1 = rx_quad_bcast<0>(m1), S1 = rx_quad_bcast<2>(m1);
+  const RFp P = rx_sub_u<FpCfg, 3>(rx_quad_bcast<1>(m1), U1);  // U2 - U1 + 3p in (p, 5p)
+  const RFp R = rx_sub_u<FpCfg, 3>(rx_quad_bcast<3>(m1), S1);  // S2 - S1 + 3p in (p, 5p)
+  // round 2: PP = P^2, RR = R^2, ZZ12 = ZZ1 ZZ2, ZZZ12 = ZZZ1 ZZZ2
+  const RFp m2 = rx_mul(rx_sel4(k, P, R, p.ZZ, p.ZZZ), rx_sel4(k, P, R, q.ZZ, q.ZZZ));
+  const RFp PP = rx_quad_bcast<0>(m2), ZZ12 = rx_quad_bcast<2>(m2);
+  // round 3: PPP = P PP, Q = U1 PP, ZZ3 = ZZ12 PP (lane 3 repeats lane 2's product)
+  const RFp m3 = rx_mul(rx_sel4(k, P, U1, ZZ12, ZZ12), PP);
+  const RFp PPP = rx_quad_bcast<0>(m3), Q = rx_quad_bcast<1>(m3);
+  G1R r;
+  r.ZZ = rx_quad_bcast<2>(m3);
+  r.X = rx_sub2_n<FpCfg, 6>(rx_quad_bcast<1>(m2), PPP, Q);  // RR + 6p - PPP - 2Q in (0, 8p)
+  // round 4: lane 0 ZZZ3 = ZZZ12 PPP (+ 0 PPP); lane 1 Y3 = R (Q - X3 + 10p) + (5p - S1) PPP
+  const RFp zero = rx_zero<FpCfg>();
+  const RFp m4 = rx_mul_add(rx_sel4(k, rx_quad_bcast<3>(m2), R, R, R),
+                            rx_sel4(k, PPP, rx_sub_u<FpCfg, 10>(Q, r.X), zero, zero),
+                            rx_sel4(k, zero, rx_sub_u<FpCfg, 5>(zero, S1), zero, zero), PPP);
+  r.ZZZ = rx_quad_bcast<0>(m4);
+  r.Y = rx_quad_bcast<1>(m4);
+  return rx_is_zero(r.ZZ) ? g1r_add_lazy_fix(p, q, r.X) : r;  // rare branch (uniform per quad)
+}
+
+// quad-cooperative chains: quad i (lanes 4i .. 4i + 3) runs the chain of thread i of k_chain
+__global__ void __launch_bounds__(256, 1) k_chain_quad(const G1xyzz* __restrict__ in, G1xyzz* __restrict__ out, int n) {
+  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  G1R acc = ld_g1r(&in[t % kPts]);
+  for (int i = 0; i < n; ++i) acc = g1r_add_lazy_quad(acc, ld_g1r(&in[(t + 7 * i + 1) % kPts]));
+  if ((threadIdx.x & 3) == 0) st_g1r(&out[t], acc);
+}
+
 __device__ __forceinline__ RFp shfl_rfp(const RFp& v, uint32_t h) {
   Fp x = rx_pack(v);
 #pragma unroll
@@ -88,7 +149,7 @@ int main() {
   for (size_t i = 0; i < (size_t)kPts * 4; ++i) h[i * 12 + 11] &= 0x0fffffffu;
   G1xyzz *din, *dout;
   CHECK(hipMalloc(&din, sizeof(G1xyzz) * kPts));
-  CHECK(hipMalloc(&dout, sizeof(G1xyzz) * 4096 * 64));
+  CHECK(hipMalloc(&dout, sizeof(G1xyzz) * 16384 * 64));  // one record per thread of the largest grid
   CHECK(hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -122,6 +183,38 @@ int main() {
     std::printf("  tree x512 workgroups: %.3f ms: %.2f us per level\n", ms, 1e3 * ms / (9 * r));
     return 0;
   };
+  // the same lone-wave chain right after a heavy full-chip kernel (as the MSM's tail runs
+  // right after k_accumulate): does the clock the heavy kernel left behind slow it down?
+  for (int rep = 0; rep < 3; ++rep) {
+    hipEvent_t a, b, c;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    CHECK(hipEventCreate(&c));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a));
+    hipLaunchKernelGGL((k_chain<1, 1>), dim3(16384), dim3(64), 0, 0, din, dout, 64);
+    CHECK(hipEventRecord(b));
+    hipLaunchKernelGGL((k_chain<1, 1>), dim3(1), dim3(64), 0, 0, din, dout, 64);
+    CHECK(hipEventRecord(c));
+    CHECK(hipEventSynchronize(c));
+    float hot = 0, lone = 0;
+    CHECK(hipEventElapsedTime(&hot, a, b));
+    CHECK(hipEventElapsedTime(&lone, b, c));
+    std::printf("after a %.2f ms full-chip chain: lone-wave chain %.2f us per dependent add\n", hot,
+                1e3 * lone / 64);
+  }
+  {  // quad-cooperative lazy addition: same values as g1r_add_lazy, time per dependent add
+    const int n = 64;
+    float ms = timeit([&] { hipLaunchKernelGGL((k_chain<1, 1>), dim3(4), dim3(64), 0, 0, din, dout, n); });
+    std::vector<uint32_t> ref(256 * 48), got(256 * 48);
+    CHECK(hipMemcpy(ref.data(), dout, ref.size() * 4, hipMemcpyDeviceToHost));
+    float mq = timeit([&] { hipLaunchKernelGGL(k_chain_quad, dim3(16), dim3(64), 0, 0, din, dout, n); });
+    CHECK(hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost));
+    std::printf("quad add: %s vs g1r_add_lazy on 256 chains; lone wave %.2f us (quads) vs %.2f us per dependent add\n",
+                ref == got ? "bit-identical" : "MISMATCH", 1e3 * mq / n, 1e3 * ms / n);
+    CHECK(hipFuncGetAttributes(&fa, (const void*)k_chain_quad));
+    std::printf("  quad chain kernel %d VGPRs (%d spill bytes)\n", fa.numRegs, (int)fa.localSizeBytes);
+  }
   if (run("g1r_add", k_chain<0, 1>, k_tree<0, 1>)) return 1;
   if (run("g1r_add_lazy", k_chain<1, 1>, k_tree<1, 1>)) return 1;
   if (run("g1r_add_lazy, 2 waves/SIMD cap", k_chain<1, 2>, k_tree<1, 2>)) return 1;
