@@ -23,7 +23,8 @@ namespace plk {
 
 namespace {
 
-constexpr uint32_t kMaxLr = 8;   // radix up to 256
+constexpr uint32_t kMaxLr = 9;   // radix up to 512 (PLK_NTT_MAX_LR: up to kMaxLrHard)
+constexpr uint32_t kMaxLrHard = 10;
 constexpr uint32_t kMaxLe = 10;  // 1024 elements (32 KiB) per workgroup
 
 __device__ __forceinline__ Fr ld_fr(const Fr* p) {
@@ -516,7 +517,18 @@ static void plan_domain(plk_domain* d) {
   uint32_t le = L > 8 ? L - 8 : 1;
   if (le < le_min) le = L < le_min ? L : le_min;
   if (le > kMaxLe) le = kMaxLe;
-  const uint32_t max_lr = le < kMaxLr ? le : kMaxLr;
+  // radix cap 2^9: 2^17 and 2^18 run in two passes of 2-column tiles (512 rows) instead of
+  // three; 2^19 and up keep three passes of >= 4 columns. Round 3 (tools/gpu_r03_lr.sh): cap
+  // 2^8 / 2^9 / 2^10 — 2^17 0.110 / 0.095 / 0.095 ms per dft + idft, 2^18 0.122 / 0.113 /
+  // 0.113, 2^20 0.31 / 0.31 / 0.34 (two passes of 1-column tiles: 32-byte strided reads);
+  // the 2^16 proof (its 2^17 coset transforms) 23.4 -> 25.9 M constraints/s.
+  // PLK_NTT_MAX_LR overrides it (up to 10).
+  static const uint32_t lr_cap = [] {
+    const char* e = getenv("PLK_NTT_MAX_LR");
+    const int v = e ? atoi(e) : (int)kMaxLr;
+    return (uint32_t)(v >= 1 && v <= (int)kMaxLrHard ? v : kMaxLr);
+  }();
+  const uint32_t max_lr = le < lr_cap ? le : lr_cap;
   const uint32_t P = (L + max_lr - 1) / max_lr;
   uint32_t lp = 0;
   for (uint32_t q = 0; q < P; ++q) {
@@ -665,10 +677,15 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     str.pre = bt.pre ? bt.pre_stride : 0;
     str.post = bt.post ? bt.post_stride : 0;
 #define PLK_LAUNCH_DS(PRE, POST, PRUNE, DS, PF)                                           \
-  hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE, DS, PF>), grid, dim3(bd), lds, stream, src, dst, tw, \
-                     ptw, pre_table ? pre_table : d->coset_pow.as<Fr>(),               \
-                     bt.post ? bt.post : d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n, \
-                     ps.lp, ps.lr, ps.lt, lin, str)
+  do {                                                                                    \
+    const void* kp_ = reinterpret_cast<const void*>(&k_ntt_pass<PRE, POST, PRUNE, DS, PF>); \
+    if (lds > 65536)                                                                      \
+      PLK_HIP_TRY(hipFuncSetAttribute(kp_, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE, DS, PF>), grid, dim3(bd), lds, stream, src, dst, \
+                       tw, ptw, pre_table ? pre_table : d->coset_pow.as<Fr>(),            \
+                       bt.post ? bt.post : d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n,  \
+                       ps.lp, ps.lr, ps.lt, lin, str);                                     \
+  } while (0)
 #define PLK_LAUNCH(PRE, POST, PRUNE)                              \
   do {                                                            \
     if (small) PLK_LAUNCH_DS(PRE, POST, PRUNE, kDSSmall, false);   \
