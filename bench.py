@@ -407,6 +407,20 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=No
             direct = json.loads(f.read_text())
         except ValueError:
             direct = None
+    # the concurrent 2^20 throughput measured directly on the GPU box (tools/cpu_node_n20.py:
+    # 16 single-thread 2^20 proofs at once, ~5 minutes, too long for every bench run)
+    node20 = None
+    f20 = ROOT / "profiles" / "r03_cpu_node_n20.json"
+    if k == 20 and f20.exists():
+        try:
+            d20 = json.loads(f20.read_text())
+            node20 = {"value": d20["window_constraints_per_s"], "unit": "constraints/s",
+                      "procs": d20["procs"], "n": d20["n"],
+                      "create_proof_s": [min(d20["create_proof_s"]), max(d20["create_proof_s"])],
+                      "window_s": d20["window_s"], "latency_16_threads_s": d20.get("latency_create_proof_s"),
+                      "source": "profiles/r03_cpu_node_n20.json (stored measurement, tools/cpu_node_n20.py)"}
+        except (ValueError, KeyError):
+            node20 = None
     out = {
         "value": conc["value"], "unit": "constraints/s", "cores": conc["procs"], "kind": "port",
         "measure": (f"MEASURED throughput of {conc['procs']} concurrent independent proofs at "
@@ -414,6 +428,7 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=No
                     "share); an upper bound of the CPU's 2^20 throughput"),
         "host": share,
         "concurrent": conc,
+        "concurrent_2_20": node20,
         "latency": {
             "value": n / per_proof, "unit": "constraints/s", "threads": threads, "n": n,
             "seconds_per_proof": per_proof, "composed": ks != k,
@@ -440,6 +455,8 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=No
         out["ratio"] = {"gpu_over_cpu_share": gpu_value / conc["value"],
                         "gpu_over_node_projection": gpu_value / out["node_projection"]["value"],
                         "gpu_over_latency": gpu_value / out["latency"]["value"]}
+        if node20:
+            out["ratio"]["gpu_over_measured_2_20_share"] = gpu_value / node20["value"]
     return out
 
 
@@ -754,19 +771,22 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
         t_idft = sum(e[1].elapsed_time(e[2]) for e in ev) / steps
         launch_ms = (t_dft + t_idft) / 2
         alg_bytes = 64.0 * n  # one read + one write of 32 B per point
-        roof = {"bound": "hbm", "kernel": "k_ntt_pass (all passes of one transform)",
-                "achieved": alg_bytes / (launch_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "traffic": load_pmc_traffic("k_ntt_pass", fname=f"pmc_traffic_ntt{k}.json"),
-                "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": launch_ms,
-                "dft_ms": t_dft, "idft_ms": t_idft,
-                # the radix-2 butterflies' Fr multiplications against the measured redundant-
-                # limb Fr multiply rate (tools/ubench_limbs.hip): the instruction-side floor
-                "valu": {"achieved": (n / 2) * k / (launch_ms * 1e-3), "peak": FR_MUL_PEAK,
-                         "unit": "Fr mul/s", "frac": (n / 2) * k / (launch_ms * 1e-3) / FR_MUL_PEAK,
-                         "peak_source": "measured by tools/ubench_limbs.hip (ffr.hpp Fr multiply, "
-                                        "whole chip)", "ops": "(N/2) log2 N butterflies"},
+        gbs = alg_bytes / (launch_ms * 1e-3) / 1e9
+        muls = (n / 2) * k / (launch_ms * 1e-3)
+        # binding roofline: the instruction side — the radix-2 butterflies' Fr multiplications
+        # (algorithmic count, (N/2) log2 N) against the measured redundant-limb Fr multiply rate
+        # (tools/ubench_limbs.hip); HBM (64 B per point) is the secondary figure under `hbm`
+        roof = {"bound": "valu", "kernel": "k_ntt_pass (all passes of one transform)",
+                "achieved": muls, "peak": FR_MUL_PEAK, "unit": "Fr mul/s", "frac": muls / FR_MUL_PEAK,
+                "peak_source": "measured by tools/ubench_limbs.hip (ffr.hpp Fr multiply, whole chip)",
+                "ops": "(N/2) log2 N butterfly multiplications per transform",
+                "traffic": load_pmc_traffic("k_ntt_pass", fname=f"pmc_traffic_ntt{k}.json"),
+                "avg_launch_ms": launch_ms, "dft_ms": t_dft, "idft_ms": t_idft,
+                "hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                        "algorithmic_bytes_per_launch": alg_bytes},
                 "note": "per transform (all its Stockham passes; traffic summed over them); "
-                        "instruction-bound, see DESIGN §3"}
+                        "instruction-bound: the lone transform's passes load, compute and store in "
+                        "lockstep, see DESIGN §3"}
         metric = f"standalone BlsScalar dft+idft points/s at n=2^{k} (BASELINE configs[1])"
         workload = f"Fft::dft + Fft::idft of one 2^{k}-point Fr vector, device-resident"
     else:
@@ -967,11 +987,14 @@ def main():
             "note": "integer-VALU-bound path (no MFMA); HBM reported as the required secondary roofline",
         },
     }
-    if kname == "k_accumulate" and acc:
+    if kname == "k_accumulate" and acc:  # the binding (VALU issue) roofline at top level
         adds = sum(hp.msm_adds) / len(hp.msm_adds)
-        result["roofline"]["point_adds_per_launch"] = adds
-        result["roofline"]["point_adds_per_s"] = adds / (launch_ms * 1e-3)
-        result["roofline"]["valu"] = valu_roofline(adds / (launch_ms * 1e-3))
+        roof = binding_roofline(valu_roofline(adds / (launch_ms * 1e-3)), achieved, alg_bytes,
+                                traffic, kname)
+        roof.update({"avg_launch_ms": launch_ms, "point_adds_per_launch": adds,
+                     "point_adds_per_s": adds / (launch_ms * 1e-3),
+                     "note": "integer-VALU-bound (no MFMA); HBM is the secondary roofline"})
+        result["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(k, hp.pp, cpu_threads(args))
     if rank == 0:

@@ -60,6 +60,8 @@ def test_kernel_mode_line_is_bit_exact(mode):
     assert d["bit_exact_vs_oracle"] is True
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 4 and cb["value"] > 0
+    # both kernels are instruction-bound: the binding (VALU) roofline at top level, HBM beside
+    assert d["roofline"]["bound"] == "valu" and d["roofline"]["hbm"]["unit"] == "GB/s"
 
 
 @pytest.mark.gpu

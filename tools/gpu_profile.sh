@@ -12,7 +12,7 @@ O=gpurun_out/prof
 rm -rf $O; mkdir -p $O/stats $O/pmc $O/bd20 $O/bd16
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py --no-cpu-baseline > $O/stats/bench.log 2>&1 || { echo PROF_FAILED; tail -30 $O/stats/bench.log; exit 1; }
 grep '"metric"' $O/stats/bench.log > $O/bench_line.json
-python3 -c "import json; d=json.load(open('$O/bench_line.json')); r=d['roofline']; print('bench', round(d['value']/1e6,3), 'M/s; k_accumulate solo', round(r['avg_launch_ms'],3), 'ms, valu', round(r['valu']['frac'],3))"
+python3 -c "import json; d=json.load(open('$O/bench_line.json')); r=d['roofline']; print('bench', round(d['value']/1e6,3), 'M/s; k_accumulate solo', round(r['avg_launch_ms'],3), 'ms, binding', r['bound'], round(r['frac'],3))"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc/$c -o run -- python3 bench.py --no-cpu-baseline > $O/pmc/$c.log 2>&1 || { echo PMC_FAILED $c; tail -20 $O/pmc/$c.log; exit 1; }
 done
