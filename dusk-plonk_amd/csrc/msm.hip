@@ -304,6 +304,101 @@ __global__ void k_make_tasks(const uint32_t* __restrict__ offsets,
         make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << kTaskShift));
 }
 
+// Small bucket sets (B <= kSortSmallMax: the 2^12-size commits, c <= 13) in ONE dispatch per
+// batch instead of three: k_block_scan + k_scan_buckets + k_make_tasks on one workgroup per
+// slot (the bucket counts and the tail-length cursors in LDS, so the tail ranks need no global
+// atomics). Small proofs are bound by the rate at which the command processor takes
+// dispatches, not by these kernels' work. The task layout is k_make_tasks' (full
+// tasks in bucket order, then the tails grouped by length, longest first).
+constexpr uint32_t kSortSmallMax = 4096;
+__global__ void __launch_bounds__(1024) k_sort_small(uint32_t* __restrict__ blockhist, uint32_t nblk,
+                                                     uint32_t B, uint32_t chunk,
+                                                     uint32_t* __restrict__ offsets,
+                                                     uint32_t* __restrict__ task_off,
+                                                     uint2* __restrict__ tasks, uint64_t task_stride) {
+  __shared__ uint32_t s_count[kSortSmallMax];
+  __shared__ uint32_t s_c[1024], s_t[1024], s_f[1024], s_len[kChunkMax], s_cur[kChunkMax];
+  const uint32_t slot = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
+  blockhist += (size_t)slot * nblk * B;
+  offsets += (size_t)slot * (B + 1);
+  task_off += (size_t)slot * (B + 1);
+  tasks += (size_t)slot * task_stride;
+  if (tid < kChunkMax) s_len[tid] = 0;
+  // per bucket, over the histogram workgroups: exclusive running counts (k_block_scan)
+  for (uint32_t b = tid; b < B; b += nt) {
+    uint32_t* h = blockhist + b;
+    uint32_t run = 0, k = 0;
+    for (; k + 8 <= nblk; k += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) v[u] = h[(size_t)(k + u) * B];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) {
+        h[(size_t)(k + u) * B] = run;
+        run += v[u];
+      }
+    }
+    for (; k < nblk; ++k) {
+      const uint32_t v = h[(size_t)k * B];
+      h[(size_t)k * B] = run;
+      run += v;
+    }
+    s_count[b] = run;
+  }
+  __syncthreads();
+  // offsets / task offsets / full-task offsets over each thread's contiguous buckets
+  // (k_scan_buckets)
+  const uint32_t per = (B + nt - 1) / nt;
+  const uint32_t b0 = min(tid * per, B), b1 = min(b0 + per, B);
+  uint32_t c_sum = 0, t_sum = 0, f_sum = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = s_count[b];
+    c_sum += c;
+    t_sum += (c + chunk - 1) / chunk;
+    f_sum += c / chunk;
+    if (c % chunk) atomicAdd(&s_len[c % chunk], 1u);
+  }
+  s_c[tid] = c_sum;
+  s_t[tid] = t_sum;
+  s_f[tid] = f_sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < nt; off <<= 1) {
+    const uint32_t a = tid >= off ? s_c[tid - off] : 0, t = tid >= off ? s_t[tid - off] : 0;
+    const uint32_t f = tid >= off ? s_f[tid - off] : 0;
+    __syncthreads();
+    s_c[tid] += a;
+    s_t[tid] += t;
+    s_f[tid] += f;
+    __syncthreads();
+  }
+  if (tid == 0) {  // tails after the full tasks, longest first
+    uint32_t run = s_f[nt - 1];
+    for (uint32_t l = chunk - 1; l >= 1; --l) {
+      s_cur[l] = run;
+      run += s_len[l];
+    }
+    offsets[B] = s_c[nt - 1];
+    task_off[B] = s_t[nt - 1];
+  }
+  __syncthreads();
+  // the task records (k_make_tasks), tail ranks from LDS cursors
+  uint32_t c_run = s_c[tid] - c_sum, t_run = s_t[tid] - t_sum, f_run = s_f[tid] - f_sum;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t cnt = s_count[b];
+    offsets[b] = c_run;
+    task_off[b] = t_run;
+    const uint32_t nfull = cnt / chunk, tail = cnt - nfull * chunk;
+    for (uint32_t t = 0; t < nfull; ++t)
+      tasks[f_run + t] = make_uint2(c_run + t * chunk, (t_run + t) | ((chunk - 1) << kTaskShift));
+    if (tail)
+      tasks[atomicAdd(&s_cur[tail], 1u)] =
+          make_uint2(c_run + nfull * chunk, (t_run + nfull) | ((tail - 1) << kTaskShift));
+    c_run += cnt;
+    t_run += (cnt + chunk - 1) / chunk;
+    f_run += nfull;
+  }
+}
+
 // ---- wide bucket sets (B > kLdsBuckets, c >= 17): two-level radix sort ----------------
 // One LDS histogram cannot hold the buckets, and per-(workgroup, bucket) runs of ~1 entry
 // make a direct scatter write-amplified. Instead: (1) coarse bins of kFine consecutive
@@ -789,6 +884,17 @@ __global__ void __launch_bounds__(256, PLK_RUNSUM_WAVES) k_runsum2(uint32_t B, u
 // (wide bucket sets) also [9] = the plain sum of the group's 256 Z values (k_runsum).
 constexpr uint32_t kBitsumOut = 10;
 
+// k_bitsum1's fold of k_bitsum2 (done == nullptr: off): per-slot arrival counters (zero
+// between batches), the readback record's bit sums and entry counts, as k_bitsum2 takes them
+struct BitsumFold {
+  uint32_t* done;
+  G1xyzz* out2;
+  const uint32_t* offsets;
+  uint32_t* entries;
+  uint32_t B, nbits, nout;
+};
+constexpr uint32_t kFoldMaxGroups = 16;
+
 // k-th of the 8 indices in [0, 16) with bit j set
 __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
   return ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
@@ -797,7 +903,8 @@ __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
 template <bool Z>
 __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
                                                                            const G1xyzz* __restrict__ zin,
-                                                                           G1xyzz* __restrict__ out) {
+                                                                           G1xyzz* __restrict__ out,
+                                                                           BitsumFold fold) {
   // the group's values (buckets or run sums Y; with Z also the 256 plain-sum values) are
   // read straight from HBM and the trees run over cross-lane shuffles: LDS holds only the
   // NS row / column sums (9 KiB instead of 105 — a resident k_bitsum1 used to keep the other
@@ -854,6 +961,39 @@ __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uin
       if (on && e < h && h < w) acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, o);
     }
     if (on && e == 0) st_g1r(&out[s], acc);
+  }
+  if (!fold.done) return;
+  // few groups (G <= kFoldMaxGroups): the slot's last workgroup to finish runs k_bitsum2's sums
+  // here (one dispatch fewer per batch; small proofs are dispatch-rate bound). Release this
+  // group's outputs, count it in, and the last one acquires the others' before reading them.
+  __shared__ uint32_t s_last;
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&fold.done[slot], 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const G1xyzz* in = out - (size_t)g * kBitsumOut;  // this slot's groups
+  const uint32_t j = tid >> 3, e = tid & 7, G = gridDim.x;
+  G1R acc = g1r_infinity();
+  if (j < fold.nout) {  // output j: 8 lanes, lane e takes the groups g = e mod 8
+    for (uint32_t gg = e; gg < G; gg += 8) {
+      const G1xyzz* v = &in[(size_t)gg * kBitsumOut];
+      if (j >= fold.nbits) {  // wide sets: the plain sums (j = nbits) and the A_g (nbits + 1)
+        acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[j == fold.nbits ? 9 : 8]));
+      } else if (j < 8) {
+        acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[j]));
+        if (j == 0) acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[8]));
+      } else if ((gg >> (j - 8)) & 1u) {
+        acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[8]));
+      }
+    }
+  }
+  acc = shfl_tree<PLK_BITSUM_LAZY>(acc, e, 8);
+  if (j < fold.nout && e == 0) st_g1r(&fold.out2[(size_t)slot * fold.nout + j], g1r_lazy_finish(acc));
+  if (tid == 0) {
+    fold.entries[slot] = fold.offsets[(size_t)slot * (fold.B + 1) + fold.B];
+    fold.done[slot] = 0;  // ready for the next batch (stream order)
   }
 }
 
@@ -981,6 +1121,11 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
     if ((st = w.bsum.alloc(slots * B * sizeof(G1xyzz)))) return st;
   }
   if ((st = w.bits1.alloc(groups * kBitsumOut * sizeof(G1xyzz)))) return st;
+  {  // k_bitsum1's fold counters: zero between batches (the last workgroup resets its slot's)
+    void* before = w.done.ptr;
+    if ((st = w.done.alloc(kMaxSlots * sizeof(uint32_t)))) return st;
+    if (w.done.ptr != before) PLK_HIP_TRY(hipMemsetAsync(w.done.ptr, 0, kMaxSlots * sizeof(uint32_t), stream));
+  }
   {  // readback record: header (flags, entry counts) then the bit sums (nout <= 32 per slot)
     void* before = w.bits2.ptr;
     if ((st = w.bits2.alloc(sizeof(ReadbackHeader) + (size_t)kMaxSlots * 32 * sizeof(G1xyzz))))
@@ -1101,23 +1246,32 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     } else {
       PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * B * 4, stream));
     }
-    hipLaunchKernelGGL(k_block_scan, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
-                       w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>(),
-                       (uint32_t*)nullptr, (uint32_t*)nullptr);
-    hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
-                       w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
-                       w.task_off.as<uint32_t>(), w.full_off.as<uint32_t>(),
-                       w.len_cur.as<uint32_t>());
+    const bool small_sort = B <= kSortSmallMax;
+    if (small_sort) {
+      hipLaunchKernelGGL(k_sort_small, dim3(1, slots), dim3(1024), 0, stream,
+                         w.blockhist.as<uint32_t>(), hist_blocks, B, chunk, w.offsets.as<uint32_t>(),
+                         w.task_off.as<uint32_t>(), w.tasks.as<uint2>(), (uint64_t)w.task_stride);
+    } else {
+      hipLaunchKernelGGL(k_block_scan, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
+                         w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>(),
+                         (uint32_t*)nullptr, (uint32_t*)nullptr);
+      hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
+                         w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
+                         w.task_off.as<uint32_t>(), w.full_off.as<uint32_t>(),
+                         w.len_cur.as<uint32_t>());
+    }
     if (max_len) {
       hipLaunchKernelGGL(k_scatter, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream,
                          batch, cfg, (uint64_t)s->n, w.offsets.as<uint32_t>(),
                          w.blockhist.as<uint32_t>(), w.sorted.as<uint32_t>(),
                          (uint64_t)w.sorted_stride);
     }
-    hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
-                       w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),
-                       w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>(), B, chunk,
-                       w.tasks.as<uint2>(), (uint64_t)w.task_stride);
+    if (!small_sort) {
+      hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
+                         w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),
+                         w.full_off.as<uint32_t>(), w.len_cur.as<uint32_t>(), B, chunk,
+                         w.tasks.as<uint2>(), (uint64_t)w.task_stride);
+    }
   }
   // start / stop events stamped by the dispatch itself (its execution, as rocprofv3 times
   // it), not by the stream: with several lanes on the GPU a stream event would also count
@@ -1155,18 +1309,30 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
                        w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
   }
+  BitsumFold fold{};  // k_bitsum2 folded into k_bitsum1 when the slots have few groups
+  if (G <= kFoldMaxGroups) {
+    fold.done = w.done.as<uint32_t>();
+    fold.out2 = bits_dev;
+    fold.offsets = w.offsets.as<uint32_t>();
+    fold.entries = hdr_dev->entries;
+    fold.B = B;
+    fold.nbits = nbits;
+    fold.nout = nout;
+  }
   if (wide) {
     hipLaunchKernelGGL(k_bitsum1<true>, dim3(G, slots), dim3(192), 0, stream, NR,
                        (const G1xyzz*)w.ys.as<G1xyzz>(), (const G1xyzz*)w.zs.as<G1xyzz>(),
-                       w.bits1.as<G1xyzz>());
+                       w.bits1.as<G1xyzz>(), fold);
   } else {
     hipLaunchKernelGGL(k_bitsum1<false>, dim3(G, slots), dim3(128), 0, stream, B,
                        (const G1xyzz*)w.bsum.as<G1xyzz>(), (const G1xyzz*)nullptr,
-                       w.bits1.as<G1xyzz>());
+                       w.bits1.as<G1xyzz>(), fold);
   }
-  hipLaunchKernelGGL(k_bitsum2, dim3(nout, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
-                     G, nbits, nout, bits_dev, (const uint32_t*)w.offsets.as<uint32_t>(), B,
-                     hdr_dev->entries);
+  if (!fold.done) {
+    hipLaunchKernelGGL(k_bitsum2, dim3(nout, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
+                       G, nbits, nout, bits_dev, (const uint32_t*)w.offsets.as<uint32_t>(), B,
+                       hdr_dev->entries);
+  }
   PLK_HIP_TRY(hipGetLastError());
 
   // ONE copy of the readback record: flags, entry counts, then the slots' bit sums

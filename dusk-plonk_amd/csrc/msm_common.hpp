@@ -88,6 +88,7 @@ struct MsmWorkspace {
       bits2;
   // wide bucket sets only (msm.hip: two-level sort, run-sum reduction)
   DevBuf tmp, task_rel, bin_tot, len_fill, coarse_off, rsum, ys, zs;
+  DevBuf done;  // k_bitsum1's per-slot arrival counters (its fold of k_bitsum2)
   PinnedBuf host_out;  // the readback record (ReadbackHeader + bit sums) on the host
   uint32_t gen = 0;    // generation number of the last batch (degree-check flag stamps)
   size_t cap_len = 0, task_stride = 0, sorted_stride = 0;

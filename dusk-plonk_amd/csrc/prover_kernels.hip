@@ -206,6 +206,46 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_tops(Fr* __restrict__ tot
   if (threadIdx.x == kScanThreads - 1) stf(&tot[nb], sh[kScanThreads - 1]);
 }
 
+// Small scans (n <= kScanSingleMax) in ONE dispatch: a workgroup of 1 024 threads, thread t
+// owning the per = ceil(n / 1024) consecutive logical elements from t * per (reduce, block
+// scan of the thread totals in LDS, apply). Small proofs are bound by the rate at which the
+// command processor takes dispatches (~140 k/s with 16 lanes), and the 3-phase
+// form is 3 of them per scan.
+constexpr uint32_t kScanSingleThreads = 1024, kScanSingleMax = 32 * kScanSingleThreads;
+// tot[nb] = the grand total, as the 3-phase form leaves it (the grand product's caller reads it)
+template <bool MUL, bool SUFFIX, bool EXCL>
+__global__ void __launch_bounds__(kScanSingleThreads) k_scan_single(const Fr* __restrict__ in,
+                                                                    uint64_t n, Fr* __restrict__ out,
+                                                                    Fr* __restrict__ tot, uint32_t nb) {
+  __shared__ Fr sh[kScanSingleThreads];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (uint32_t)((n + kScanSingleThreads - 1) / kScanSingleThreads);
+  const uint64_t base = (uint64_t)tid * per;
+  Fr acc = ident<MUL>();
+  for (uint32_t k = 0; k < per && base + k < n; ++k) acc = op<MUL>(acc, ldf(&in[phys<SUFFIX>(base + k, n)]));
+  sh[tid] = acc;
+  __syncthreads();
+  for (uint32_t off = 1; off < kScanSingleThreads; off <<= 1) {
+    Fr v = tid >= off ? sh[tid - off] : ident<MUL>();
+    __syncthreads();
+    sh[tid] = op<MUL>(sh[tid], v);
+    __syncthreads();
+  }
+  Fr run = tid ? sh[tid - 1] : ident<MUL>();
+  if (tid == kScanSingleThreads - 1) stf(&tot[nb], sh[tid]);
+  for (uint32_t k = 0; k < per && base + k < n; ++k) {
+    const uint64_t p = phys<SUFFIX>(base + k, n);
+    const Fr v = ldf(&in[p]);
+    if (EXCL) {
+      stf(&out[p], run);
+      run = op<MUL>(run, v);
+    } else {
+      run = op<MUL>(run, v);
+      stf(&out[p], run);
+    }
+  }
+}
+
 template <bool MUL, bool SUFFIX, bool EXCL>
 __global__ void __launch_bounds__(kScanThreads) k_scan_apply(const Fr* __restrict__ in, uint64_t n,
                                                              const Fr* __restrict__ tot,
@@ -488,6 +528,64 @@ __global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restric
   if (threadIdx.x == 0) stf(&out[k], sh[0]);
 }
 
+// Ruffini for small polynomials (len <= kRuffiniSingleMax) in ONE dispatch instead of five
+// (pk_ruffini: scale powers, 3-phase scan, scale powers): q_k = z^-(k+1) sum_(i>k) c_i z^i.
+// A workgroup of 1 024 threads; thread t owns j in [tE, tE + E) (E = ceil(len / 1024) <= 16).
+// Pass 1 (upward) forms y_j = c_j z^j and the thread's sum; an exclusive suffix scan of the
+// sums over the threads (LDS) gives each thread the sum of y above its range; pass 2 walks
+// its range downward with that running sum. Start powers z^(tE) and z^-(tE+1) come from
+// product scans of z^E / z^-E in LDS. All powers R'-domain (the host converts), products in
+// the R domain, outputs canonical: the same field values as the five-dispatch form.
+constexpr uint32_t kRuffiniThreads = 1024, kRuffiniSingleMax = 16 * kRuffiniThreads;
+__global__ void __launch_bounds__(kRuffiniThreads) k_ruffini_single(const Fr* __restrict__ c, uint64_t len,
+                                                                    uint32_t E, Fr z, Fr zE, Fr zi,
+                                                                    Fr ziE, Fr* __restrict__ q) {
+  __shared__ Fr T[kRuffiniThreads], U[kRuffiniThreads];
+  const uint32_t tid = threadIdx.x;
+  T[tid] = tid ? zE : rx_pack(rx_one<FrCfg>());
+  U[tid] = tid ? ziE : zi;
+  __syncthreads();
+  for (uint32_t h = 1; h < kRuffiniThreads; h <<= 1) {  // inclusive product scans
+    const RFr a = tid >= h ? rx_unpack(T[tid - h]) : rx_one<FrCfg>();
+    const RFr b = tid >= h ? rx_unpack(U[tid - h]) : rx_one<FrCfg>();
+    __syncthreads();
+    if (tid >= h) {
+      T[tid] = rx_pack(rx_mul(rx_unpack(T[tid]), a));
+      U[tid] = rx_pack(rx_mul(rx_unpack(U[tid]), b));
+    }
+    __syncthreads();
+  }
+  const uint64_t j0 = (uint64_t)tid * E;
+  const uint64_t j1 = j0 + E < len ? j0 + E : (j0 < len ? len : j0);
+  const RFr zr = rx_unpack(z), zir = rx_unpack(zi);
+  RFr pw = rx_unpack(T[tid]);   // z^j0
+  RFr pwi = rx_unpack(U[tid]);  // z^-(j0 + 1)
+  Fr loc = fe_zero<FrCfg>();
+  for (uint64_t j = j0; j < j1; ++j) {  // pass 1: this thread's sum of y_j
+    loc = fe_add(loc, rx_pack_canonical(rx_mul(ldr(&c[j]), pw)));
+    pw = rx_mul(pw, zr);
+    pwi = rx_mul(pwi, zir);
+  }
+  __syncthreads();  // T free again
+  T[tid] = loc;
+  __syncthreads();
+  for (uint32_t h = 1; h < kRuffiniThreads; h <<= 1) {  // inclusive suffix sums over threads
+    const Fr o = tid + h < kRuffiniThreads ? T[tid + h] : fe_zero<FrCfg>();
+    __syncthreads();
+    T[tid] = fe_add(T[tid], o);
+    __syncthreads();
+  }
+  Fr run = fe_sub(T[tid], loc);  // sum of y_i over i >= j1
+  // pass 2, downward from j1 - 1: pw = z^j1 -> z^k, pwi = z^-(j1 + 1) -> z^-(k + 1)
+  for (uint64_t k = j1; k-- > j0;) {
+    pw = rx_mul(pw, zir);
+    pwi = rx_mul(pwi, zr);
+    const Fr yk = rx_pack_canonical(rx_mul(ldr(&c[k]), pw));  // read before q[k] (q may be c)
+    if (k + 1 < len) stf(&q[k], rx_pack_canonical(rx_mul(rx_unpack(run), pwi)));
+    run = fe_add(run, yk);
+  }
+}
+
 // ---------------------------------------------------------------- linear combos
 // out[j] = sum_t s_t * p_t[j] (p_t[j] = 0 past len_t), j < len_out
 // (redundant limbs: the scalars arrive in the R' domain, pk_lincomb)
@@ -594,12 +692,18 @@ int pk_scan(const Fr* in, Fr* out, uint64_t n, bool mul, bool suffix, bool exclu
             hipStream_t s) {
   if (n == 0) return PLK_OK;
   const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
-#define SCAN3(M, S, E)                                                                         \
-  do {                                                                                         \
-    hipLaunchKernelGGL((k_scan_reduce<M, S>), dim3(nb), dim3(kScanThreads), 0, s, in, n, tmp); \
-    hipLaunchKernelGGL((k_scan_tops<M>), dim3(1), dim3(kScanThreads), 0, s, tmp, nb);          \
-    hipLaunchKernelGGL((k_scan_apply<M, S, E>), dim3(nb), dim3(kScanThreads), 0, s, in, n, tmp, \
-                       out);                                                                   \
+  const bool single = n <= kScanSingleMax;
+#define SCAN3(M, S, E)                                                                           \
+  do {                                                                                           \
+    if (single) {                                                                                \
+      hipLaunchKernelGGL((k_scan_single<M, S, E>), dim3(1), dim3(kScanSingleThreads), 0, s, in, n, \
+                         out, tmp, nb);                                                          \
+      break;                                                                                     \
+    }                                                                                            \
+    hipLaunchKernelGGL((k_scan_reduce<M, S>), dim3(nb), dim3(kScanThreads), 0, s, in, n, tmp);   \
+    hipLaunchKernelGGL((k_scan_tops<M>), dim3(1), dim3(kScanThreads), 0, s, tmp, nb);            \
+    hipLaunchKernelGGL((k_scan_apply<M, S, E>), dim3(nb), dim3(kScanThreads), 0, s, in, n, tmp,   \
+                       out);                                                                     \
   } while (0)
   if (mul) {
     if (suffix) {
@@ -689,6 +793,15 @@ int pk_ruffini(const Fr* c, uint64_t len, const Fr& z, Fr* q, Fr* tmp, Fr* scan_
                hipStream_t s) {
   if (len <= 1) return PLK_OK;
   int st;
+  if (len <= kRuffiniSingleMax) {  // one dispatch (k_ruffini_single)
+    const uint32_t E = (uint32_t)((len + kRuffiniThreads - 1) / kRuffiniThreads);
+    const Fr zinv = fe_inv(z);
+    hipLaunchKernelGGL(k_ruffini_single, dim3(1), dim3(kRuffiniThreads), 0, s, c, len, E,
+                       fe_to_rx_domain(z), fe_to_rx_domain(fe_pow_u64(z, E)), fe_to_rx_domain(zinv),
+                       fe_to_rx_domain(fe_pow_u64(zinv, E)), q);
+    PLK_HIP_TRY(hipGetLastError());
+    return PLK_OK;
+  }
   if ((st = pk_scale_powers(c, len, z, 0, tmp, s))) return st;          // y_j = c_j z^j
   if ((st = pk_scan(tmp, tmp, len, false, true, true, scan_tmp, s))) return st;  // S_j = sum_{i>j} y_i
   const Fr zinv = fe_inv(z);

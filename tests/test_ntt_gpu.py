@@ -181,3 +181,46 @@ def test_zero_padded_first_pass(plk, gpu_ctx, oracle, k):
         assert np.array_equal(f.dft(plk.Coefficients(xm)).values, oracle.dft(xm, k)), (k, m)
         assert np.array_equal(f.coset_dft(plk.Coefficients(xm)).values,
                               oracle.coset_dft(xm, k)), (k, m)
+
+
+_OPT_IN_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/tests"]
+import dusk_plonk_amd as plk
+from oracle_lib import random_fr
+ctx = plk.Context.default(0)
+out = {}
+for k in (16, 18, 20):
+    f = plk.Fft(k, ctx)
+    x = random_fr(1 << k, seed=900 + k)
+    out[f"x{k}"] = x
+    out[f"dft{k}"] = f.dft(plk.Coefficients(x)).values
+    out[f"idft{k}"] = f.idft(plk.PointsValue(x)).values
+    out[f"cdft{k}"] = f.coset_dft(plk.Coefficients(x[: (3 << k) // 4])).values
+    out[f"cidft{k}"] = f.coset_idft(plk.PointsValue(x)).values
+np.savez(sys.argv[2], **out)
+"""
+
+
+def test_opt_in_plans_vs_oracle(tmp_path, oracle):
+    """The opt-in NTT plans (process-wide environment switches, so in a child process): the
+    persistent software-pipelined pass (PLK_NTT_PF, several tiles per workgroup) and radix
+    up to 2^10 (PLK_NTT_MAX_LR: 2^18 / 2^20 in two passes, 1-column tiles, > 64 KiB of LDS
+    for the pruned first pass) — bit-exact against the oracle like the default plans."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    f = tmp_path / "out.npz"
+    env = dict(os.environ, PLK_NTT_PF="16", PLK_NTT_MAX_LR="10")
+    subprocess.run([sys.executable, "-c", _OPT_IN_SCRIPT, str(root), str(f)], env=env, check=True,
+                   timeout=240)
+    d = np.load(f)
+    for k in (16, 18, 20):
+        x = d[f"x{k}"]
+        assert np.array_equal(d[f"dft{k}"], oracle.ntt(x, k, 1, False)), k
+        assert np.array_equal(d[f"idft{k}"], oracle.ntt(x, k, -1, False)), k
+        assert np.array_equal(d[f"cdft{k}"], oracle.coset_dft(x[: (3 << k) // 4], k)), k
+        assert np.array_equal(d[f"cidft{k}"], oracle.ntt(x, k, -1, True)), k
