@@ -208,9 +208,15 @@ struct NttBatch {
   uint64_t pre_stride = 0;
   const Fr* post = nullptr;
   uint64_t post_stride = 0;
+  // group > 0: vector v = g * group + m reads in + g * in_group_stride + m * in_stride and its
+  // pre / post tables at m * pre_stride / m * post_stride (several polynomials' coset blocks in
+  // one launch); outputs stay at v * out_stride
+  uint32_t group = 0;
+  uint64_t in_group_stride = 0;
 };
 struct NttStrides {  // kernel-side view
-  uint64_t in, out, pre, post;
+  uint64_t in, out, pre, post, in_group;
+  uint32_t group_in, group_post;  // grouping of the first pass' inputs / the last pass' post table
 };
 int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, int coset,
                   Fr* scratch, hipStream_t stream, uint32_t count, const NttBatch& b);

@@ -265,11 +265,15 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   uint32_t* twl = smem32 + kL * DS;
   uint32_t* ztab = twl + kL * TS;   // kZTab (reduce_q)
 
-  // vector blockIdx.y of a batch: its input, output and scale-table rows
-  in += (size_t)blockIdx.y * str.in;
-  out += (size_t)blockIdx.y * str.out;
-  if (PRE == 1) pre += (size_t)blockIdx.y * str.pre;
-  if (POST == 2) post += (size_t)blockIdx.y * str.post;
+  // vector blockIdx.y of a batch: its input, output and scale-table rows (NttBatch::group)
+  {
+    const uint32_t y = blockIdx.y;
+    const uint32_t yi = str.group_in ? y % str.group_in : y, gi = str.group_in ? y / str.group_in : 0;
+    in += (size_t)yi * str.in + (size_t)gi * str.in_group;
+    out += (size_t)y * str.out;
+    if (PRE == 1) pre += (size_t)yi * str.pre;
+    if (POST == 2) post += (size_t)(str.group_post ? y % str.group_post : y) * str.post;
+  }
 
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   const uint32_t nr_log = log_n - lr;  // log2(N/R)
@@ -628,11 +632,19 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     return PLK_OK;
   }
   int st;
+  const size_t P = d->plan.size();
+  // when the output does not overlap the input, it doubles as one of the ping-pong buffers
+  // (passes alternate so the last one lands in it): a batch then needs count * n of scratch
+  // instead of 2 count n (the prover's batch of the four wires' 12 coset blocks)
+  const uint64_t in_ext = bt.group ? (uint64_t)(count / bt.group - 1) * bt.in_group_stride +
+                                         (uint64_t)(bt.group - 1) * bt.in_stride + len_in
+                                   : (uint64_t)(count - 1) * bt.in_stride + len_in;
+  const uint64_t out_ext = (uint64_t)(count - 1) * bt.out_stride + n;
+  const bool out_pp = P >= 2 && bt.out_stride >= n && (len_in == 0 || in + in_ext <= out || out + out_ext <= in);
   if (!scratch) {
     if ((st = d->scratch.alloc(2 * n * sizeof(Fr) * (count > 1 ? count : 1)))) return st;
     scratch = d->scratch.as<Fr>();
   }
-  const size_t P = d->plan.size();
   Fr* s1 = scratch;
   Fr* s2 = scratch + n * count;
   const Fr* tw = dir > 0 ? d->tw_fwd_rx.as<Fr>() : d->tw_inv.as<Fr>();
@@ -642,7 +654,7 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
   const Fr* src = no_input ? tw : in;
   for (size_t q = 0; q < P; ++q) {
     const NttPass& ps = d->plan[q];
-    Fr* dst = (q + 1 == P) ? out : ((q & 1) ? s2 : s1);
+    Fr* dst = (q + 1 == P) ? out : out_pp ? (((P - 1 - q) & 1) ? s1 : out) : ((q & 1) ? s2 : s1);
     const bool first = q == 0, last = q + 1 == P;
     const uint32_t E = 1u << (ps.lr + ps.lt);
     uint32_t bd = E / 4;
@@ -676,6 +688,9 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     str.out = last ? bt.out_stride : n * 1;
     str.pre = bt.pre ? bt.pre_stride : 0;
     str.post = bt.post ? bt.post_stride : 0;
+    str.in_group = first && !no_input ? bt.in_group_stride : 0;
+    str.group_in = first ? bt.group : 0;
+    str.group_post = last ? bt.group : 0;
 #define PLK_LAUNCH_DS(PRE, POST, PRUNE, DS, PF)                                           \
   do {                                                                                    \
     const void* kp_ = reinterpret_cast<const void*>(&k_ntt_pass<PRE, POST, PRUNE, DS, PF>); \

@@ -1030,7 +1030,9 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     TRY(P->tmp_a.alloc(5 * n * sizeof(Fr)));
     TRY(P->eval_partial.alloc((size_t)kMaxEval * pk_eval_max_blocks(nq) * sizeof(Fr)));
     TRY(P->eval_out.alloc(kMaxEval * sizeof(Fr)));
-    TRY(P->ntt_scratch.alloc(2 * nq * sizeof(Fr)));
+    // 4 nq: the four wires' 12 coset blocks transform in one batch (24n of scratch: the output
+    // doubles as the other ping-pong buffer, ntt_run_batch)
+    TRY(P->ntt_scratch.alloc(4 * nq * sizeof(Fr)));
     Fr* nsc = P->ntt_scratch.as<Fr>();
 
     // transcript seeded like Prover::new (prover.rs:54-55): Transcript::base(label, vk, m)
@@ -1071,10 +1073,15 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     Fr* wl = P->wires_lag.as<Fr>();
     Fr* wc = P->wires_coef.as<Fr>();
     TRY(pk_gather_wires(P->witness.as<Fr>(), key->wire_idx.as<uint32_t>(), m, n, wl, s));
+    {  // the four wire idfts as one batch (one launch per pass instead of four)
+      NttBatch b;
+      b.in_stride = n;
+      b.out_stride = S;
+      TRY(ntt_run_batch(key->dom, wl, wc, n, -1, 0, nsc, s, 4, b));
+    }
     BlindBatch bb{};
     bb.npoly = 4;
     for (int c = 0; c < 4; ++c) {
-      TRY(ntt_run(key->dom, wl + c * n, wc + c * S, n, -1, 0, nsc, s, 1));
       bb.poly[c] = wc + c * S;  // blind(1): b(X)(X^n - 1), two scalars per wire, drawn in order
       bb.b[c].count = 2;
       bb.b[c].r[0] = rng.fr();
@@ -1161,7 +1168,16 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     TRY(coset_fwd(zc, ev + 0 * nq, n + 3, key->coset_s));
     // wire evaluations at exponent -1 and PI at +1 for k_quotient's redundant-form
     // arithmetic (QuotientArgs): scaled coset tables, no extra pass
-    for (int c = 0; c < 4; ++c) TRY(coset_fwd(wc + c * S, ev + (1 + c) * nq, n + 2, key->coset_w));
+    {  // the four wires' coset blocks as ONE batch of 12 (NttBatch::group: wire c, block m)
+      NttBatch b;
+      b.group = kQBlocks;
+      b.in_stride = 0;
+      b.in_group_stride = S;
+      b.out_stride = n2;
+      b.pre = key->coset_w.as<Fr>();
+      b.pre_stride = n + 8;
+      TRY(ntt_run_batch(key->domq, wc, ev + nq, n + 2, 1, 1, nsc, s, 4 * kQBlocks, b));
+    }
     // PI(X) over the coset; a circuit without public inputs has PI = 0 (the term is skipped)
     if (!pis.empty()) TRY(coset_fwd(P->pi_coef.as<Fr>(), ev + 5 * nq, n, key->coset_pi));
     const Fr alpha2 = fe_sqr(alpha);

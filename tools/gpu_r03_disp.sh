@@ -11,10 +11,11 @@ timeout -k 10 900 python3 -u -m pytest tests/ -x -q --timeout 300 --timeout-meth
 tail -1 $O/pytest.log
 summ='import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e6,3), "M/s", round(d["ms_per_step"],3), "ms/step")'
 for rep in 1 2; do
-  for k in 12 14 16; do
+  for k in 12 14 16 20; do
     for lib in new prev; do
       l=""; [ $lib = prev ] && l=$PWD/dusk-plonk_amd/libplk-prev.so
-      PLK_LIB=$l timeout -k 10 300 python3 bench.py --no-cpu-baseline --log-n $k --steps 16 --warmup 3 > $O/b${k}_${lib}_$rep.log 2>&1 || { echo BENCH_FAILED; tail -20 $O/b${k}_${lib}_$rep.log; exit 1; }
+      st=16; [ $k = 20 ] && st=6
+      PLK_LIB=$l timeout -k 10 300 python3 bench.py --no-cpu-baseline --log-n $k --steps $st --warmup 3 > $O/b${k}_${lib}_$rep.log 2>&1 || { echo BENCH_FAILED; tail -20 $O/b${k}_${lib}_$rep.log; exit 1; }
       echo -n "2^$k $lib #$rep: "; grep '"metric"' $O/b${k}_${lib}_$rep.log | python3 -c "$summ"
     done
   done
