@@ -68,6 +68,11 @@ constexpr uint32_t kDSSmall = 256;
 #define PLK_NTT_FUSE 0
 #endif
 constexpr bool kFuseFirstStep = PLK_NTT_FUSE != 0;
+// -DPLK_NTT_R2FIRST=0: odd-radix passes end in a stage of half 1 of their own (round 2 form)
+#ifndef PLK_NTT_R2FIRST
+#define PLK_NTT_R2FIRST 1
+#endif
+constexpr bool kR2First = PLK_NTT_R2FIRST != 0;
 // k_ntt_pass minimum waves per SIMD (-DPLK_NTT_MINW=4 caps it at 128 VGPRs)
 #ifndef PLK_NTT_MINW
 #define PLK_NTT_MINW 1
@@ -327,7 +332,13 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   int lh = (int)lr - 1 - (PRUNE ? 3 : 0);
   // first radix-4 step fused into the load phase (uniform): a thread's four elements form
   // one of its groups when E = 4 bd
-  const bool fuse = kFuseFirstStep && !PRUNE && lr >= 2 && E == 4 * bd;
+  const bool fuse = kFuseFirstStep && !PRUNE && lr >= 2 && E == 4 * bd && !(lr & 1);
+  // odd radix: the first radix-2 stage (half R/2) runs on the loaded registers — a thread's
+  // elements c and c + nit/2 are rows j and j + R/2 of one column when E >= 2 bd — and the
+  // remaining even count of stages ends in the twiddle-free radix-4 step of halves (2, 1),
+  // instead of a last stage of half 1 in its own LDS round trip (one round trip and barrier
+  // fewer, R/4 fewer products per column)
+  const bool r2first = !PRUNE && kR2First && (lr & 1) && lr >= 3 && E >= 2 * bd;
   if (PRUNE) {
     __syncthreads();
     // item = (row j < R/8, column t, half hs): blocks 4 hs .. 4 hs + 3 of (j, t)
@@ -368,7 +379,9 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
         v = rx_unpack(raw[c]);
         if (PRE == 1) v = rx_mul(v, rx_unpack(aux[c]));
       }
-      if (PRE != 1 && lp != 0 && j != 0 && (i & (p - 1)) != 0) v = rx_mul(v, rx_unpack(aux[c]));
+      // inter-pass twiddle: unconditional (the j = 0 / k = 0 entries are one; a wave's lanes
+      // all multiply anyway, and the lane-dependent skip cost registers)
+      if (PRE != 1 && lp != 0) v = rx_mul(v, rx_unpack(aux[c]));
       return v;
     };
     if (fuse) {
@@ -382,13 +395,27 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
                   ((j + 2 * h) << lt) + t, ((j + 3 * h) << lt) + t, x0, x1, x2, x3);
       lh -= 2;
     } else {
+      // element e = tid + c bd sits at LDS index e = (row << lt) + column. With r2first the
+      // upper half's elements (c >= nit / 2: rows j + R/2) meet their partner, which this
+      // thread stored at e - E/2 one iteration earlier (read back without a barrier), and the
+      // pair's butterfly is stored in place. One loop for both forms: as two code paths the
+      // compiler hoisted all four inputs above the branch (137 VGPRs instead of 115)
+      if (r2first) __syncthreads();  // twl / ztab staged
 #pragma unroll
       for (uint32_t c = 0; c < kLoadIt; ++c) {
         if (c >= nit) break;
         const uint32_t e = tid + c * bd;
-        const RFr v = input(c);
-        if (e < E) lds_std<DS>(data, ((e >> lt) << lt) + (e & (T - 1)), v);
+        const RFr v = input(c);  // < 2r, normalised
+        if (r2first && 2 * c >= nit) {
+          const uint32_t el = e - (E >> 1);
+          const RFr a = lds_ldd<DS>(data, el);
+          lds_std<DS>(data, el, reduce_q(add_u(a, v), ztab));                        // < 1.6r
+          lds_std<DS>(data, e, rx_mul(sub_u(a, v), lds_ld(twl, TS, el >> lt)));      // < 2r
+        } else if (e < E) {
+          lds_std<DS>(data, e, v);
+        }
       }
+      if (r2first) lh -= 1;
     }
     if (PF && tile + gridDim.x < nblk) issue((tile + gridDim.x) << lt);  // next tile's loads
   }
