@@ -1003,6 +1003,10 @@ __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uin
 // Also the batch's readback record (ReadbackHeader): workgroup (0, slot) copies the slot's
 // entry count (its point additions, offsets[B]) next to the flags k_any_nonzero stamped, so
 // the host reads flags, counts and bit sums with ONE copy.
+// k_bitsum2's additions: lazy (PLK_BITSUM2_LAZY=1) or the branching g1r_add
+#ifndef PLK_BITSUM2_LAZY
+#define PLK_BITSUM2_LAZY 1
+#endif
 __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, uint32_t nout,
                                                  G1xyzz* __restrict__ out,
@@ -1027,24 +1031,24 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
     for (uint32_t i : {i0, i1}) {
       if (i == kBitsumOut) continue;
       const G1R v = ld_g1r(&e[i]);
-      if (have) acc = g1r_add_lazy(acc, v);
+      if (have) acc = g1r_add_t<PLK_BITSUM2_LAZY>(acc, v);
       else acc = v;
       have = true;
     }
   }
   // lanes >= G hold infinity: a shuffle tree over each wave's min(G, 64) lanes, then the
   // wave totals through LDS (768 B instead of a 48 KiB tree)
-  acc = shfl_tree<true>(acc, tid & 63, min(G, 64u));
+  acc = shfl_tree<PLK_BITSUM2_LAZY>(acc, tid & 63, min(G, 64u));
   const uint32_t nw = min(G, 256u) > 64 ? min(G, 256u) >> 6 : 1;  // waves holding values
   if ((tid & 63) == 0 && (tid >> 6) < nw) st_g1r(&sh[tid >> 6], acc);
   __syncthreads();
   if (tid < 2) {  // the (up to) 4 wave totals as a 2-level tree: lanes 0 / 1 add a pair each
     acc = 2 * tid < nw ? ld_g1r(&sh[2 * tid]) : g1r_infinity();
-    if (2 * tid + 1 < nw) acc = g1r_add_lazy(acc, ld_g1r(&sh[2 * tid + 1]));
+    if (2 * tid + 1 < nw) acc = g1r_add_t<PLK_BITSUM2_LAZY>(acc, ld_g1r(&sh[2 * tid + 1]));
   }
   if (tid < 64) {  // wave 0 whole: the shuffle reads lane 1
     const G1R o = shfl_down_g1r(acc, 1);
-    if (tid == 0) st_g1r(&out[(size_t)slot * nout + j], g1r_lazy_finish(nw > 2 ? g1r_add_lazy(acc, o) : acc));
+    if (tid == 0) st_g1r(&out[(size_t)slot * nout + j], g1r_lazy_finish(nw > 2 ? g1r_add_t<PLK_BITSUM2_LAZY>(acc, o) : acc));
   }
 }
 
