@@ -80,7 +80,10 @@ def test_sigma_encoding_on_gpu_elements(plk, gpu_ctx):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("k", [18, 20, 23])
+# every plan shape past 2^16: 2^17 / 2^18 two passes (9 + 8, 9 + 9), 2^19 7 + 6 + 6, 2^20
+# 7 + 7 + 6, 2^21 7 + 7 + 7 (an odd radix in every pass: the radix-2 stage on the loaded
+# registers in each), 2^22 8 + 7 + 7, 2^23 8 + 8 + 7
+@pytest.mark.parametrize("k", [17, 18, 19, 20, 21, 22, 23])
 def test_large_properties(plk, gpu_ctx, oracle, k):
     import pyref as P
     n = 1 << k
