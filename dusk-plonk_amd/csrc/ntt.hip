@@ -73,6 +73,13 @@ constexpr bool kFuseFirstStep = PLK_NTT_FUSE != 0;
 #define PLK_NTT_R2FIRST 1
 #endif
 constexpr bool kR2First = PLK_NTT_R2FIRST != 0;
+// -DPLK_NTT_R4FIRST=1: even-radix passes run their first radix-4 step in the input loop (127
+// VGPRs, parity-green; measured 2^20 dft + idft 0.309-0.312 against 0.302-0.304 ms, 2^23 and
+// proofs within noise, profiles/r03_ntt_r4first_ab.txt): off
+#ifndef PLK_NTT_R4FIRST
+#define PLK_NTT_R4FIRST 0
+#endif
+constexpr bool kR4First = PLK_NTT_R4FIRST != 0;
 // k_ntt_pass minimum waves per SIMD (-DPLK_NTT_MINW=4 caps it at 128 VGPRs)
 #ifndef PLK_NTT_MINW
 #define PLK_NTT_MINW 1
@@ -339,6 +346,10 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   // instead of a last stage of half 1 in its own LDS round trip (one round trip and barrier
   // fewer, R/4 fewer products per column)
   const bool r2first = !PRUNE && kR2First && (lr & 1) && lr >= 3 && E >= 2 * bd;
+  // even radix, E = 4 bd: a thread's four elements are one group of the first radix-4 step
+  // (rows j + c R/4); the last one meets the other three, read back from the thread's own
+  // LDS slots, and the step runs in the input loop (no registers held across the loads)
+  const bool r4first = !PRUNE && kR4First && !fuse && !(lr & 1) && lr >= 4 && E == 4 * bd;
   if (PRUNE) {
     __syncthreads();
     // item = (row j < R/8, column t, half hs): blocks 4 hs .. 4 hs + 3 of (j, t)
@@ -400,13 +411,19 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
       // thread stored at e - E/2 one iteration earlier (read back without a barrier), and the
       // pair's butterfly is stored in place. One loop for both forms: as two code paths the
       // compiler hoisted all four inputs above the branch (137 VGPRs instead of 115)
-      if (r2first) __syncthreads();  // twl / ztab staged
+      if (r2first || r4first) __syncthreads();  // twl / ztab staged
 #pragma unroll
       for (uint32_t c = 0; c < kLoadIt; ++c) {
         if (c >= nit) break;
         const uint32_t e = tid + c * bd;
         const RFr v = input(c);  // < 2r, normalised
-        if (r2first && 2 * c >= nit) {
+        if (r4first && c == 3) {
+          const uint32_t t = tid & (T - 1), j = tid >> lt, h = R >> 2;
+          const RFr x0 = lds_ldd<DS>(data, e - 3 * bd), x1 = lds_ldd<DS>(data, e - 2 * bd);
+          const RFr x2 = lds_ldd<DS>(data, e - bd);
+          r4_step<DS>(data, twl, TS, ztab, j, h, 0, 1, (j << lt) + t, ((j + h) << lt) + t,
+                      ((j + 2 * h) << lt) + t, ((j + 3 * h) << lt) + t, x0, x1, x2, v);
+        } else if (r2first && 2 * c >= nit) {
           const uint32_t el = e - (E >> 1);
           const RFr a = lds_ldd<DS>(data, el);
           lds_std<DS>(data, el, reduce_q(add_u(a, v), ztab));                        // < 1.6r
@@ -416,6 +433,7 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
         }
       }
       if (r2first) lh -= 1;
+      if (r4first) lh -= 2;
     }
     if (PF && tile + gridDim.x < nblk) issue((tile + gridDim.x) << lt);  // next tile's loads
   }
