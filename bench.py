@@ -249,7 +249,8 @@ class ProofLane:
         self.base = base
         self.lane = base.prover.lane()
         self.seed = seed
-        self.synth_s, self.prove_s = [], []
+        self.synth_s, self.prove_s, self.synth_all = [], [], []
+        self.last = None  # (seed, raw proof bytes) of this lane's latest proof
         self.pool = cf.ThreadPoolExecutor(1)
         self.next = self.pool.submit(self._synth, self.seed + 1)
 
@@ -265,10 +266,50 @@ class ProofLane:
         t1 = time.perf_counter()
         proof, pi = self.lane.prove_composer(cs, self.seed)
         t2 = time.perf_counter()
+        self.synth_all.append(ts)
+        self.last = (self.seed, proof.raw_bytes())
         if timed:
             self.synth_s.append(ts)
             self.prove_s.append(t2 - t1)
         return proof
+
+
+def recheck_proofs(lanes, checker) -> tuple[int, list]:
+    """The credited configuration checked byte for byte: every lane's last timed proof
+    (circuit and blinding from its seed) proved again on `checker` with no other lane
+    running. A race between concurrent lanes (shared window table, per-lane workspaces,
+    readback stamps) would make the concurrent proof differ from the lone one."""
+    bad = []
+    for ln in lanes:
+        seed, got = ln.last
+        cs = bench_circuit(ln.base.Plonk, ln.base.chain, seed)
+        want = checker.lane.prove_composer(cs, seed)[0].raw_bytes()
+        if want != got:
+            bad.append(seed)
+    return len(lanes), bad
+
+
+def host_core_budget(torch, dist, world, lanes, step_s, device):
+    """Host cores the proof server needs against the cores it has: per rank, each lane's
+    synthesis (measured in the warmup) runs once per step beside the GPU work, so a rank
+    needs lanes x synth_s / step_s cores; summed over the node's ranks and compared with the
+    node's usable cores (affinity mask / cgroup quota). Returns (needed_per_rank,
+    needed_node, available_node) — identical on every rank."""
+    ts = [s for ln in lanes for s in ln.synth_all]
+    synth = float(np.mean(ts)) if ts else 0.0
+    need = len(lanes) * synth / max(step_s, 1e-9)
+    share = cpu_share()
+    avail = share["cgroup_quota_cpus"] or share["affinity"]
+    avail = min(avail, share["affinity"]) if avail else share["affinity"]
+    node = need
+    if world > 1:
+        on = device if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([need, -float(avail)], dtype=torch.float64, device=on)
+        dist.all_reduce(t[:1])
+        m = t[1:].clone()
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)  # the smallest report, negated
+        node, avail = float(t[0].item()), -float(m.item())
+    return need, node, avail
 
 
 def cpu_baseline(k: int, pp, threads: int):
@@ -601,14 +642,24 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
         for f in [drivers.submit(one, ln) for ln in (which or lanes)]:
             f.result()
 
+    tw = time.perf_counter()
     run(args.warmup, False)
     torch.cuda.synchronize()
+    # host cores: each lane synthesises one fresh witness per step beside the GPU work. If the
+    # node's ranks would need more cores than the node has, prove with fewer lanes per rank
+    # rather than oversubscribe (the same count on every rank: the figures are all-reduced)
+    warm_step = (time.perf_counter() - tw) / max(1, args.warmup)
+    need, need_node, avail_node = host_core_budget(torch, dist, world, lanes, warm_step, device)
+    L_run = L
+    if args.warmup and need_node > 0.9 * avail_node:
+        L_run = max(1, int(L * 0.9 * avail_node / need_node))
+    active = lanes[:L_run]
     for ln in lanes:
         ln.lane.msm_stats(reset=True)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    run(args.steps, True)
+    run(args.steps, True, active)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -616,6 +667,7 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
     if world > 1:
         elapsed = max_over_ranks(torch, dist, elapsed, device)
     steps = args.steps
+    lanes_all, lanes, L = lanes, active, L_run
     # k_accumulate inside the workload (all lanes' launches; they share the chip) ...
     acc_ms = launches = adds = points = 0
     for ln in lanes:
@@ -627,6 +679,9 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
     torch.cuda.synchronize()
     s_ms, s_l, s_a, s_p = lanes[0].lane.msm_stats(reset=True)
     cbits = base.pp.last_msm_stats()[2]
+    # every lane's last timed proof, re-proved alone on lane 0 and compared byte for byte
+    # (under --shard-msm every rank re-proves the same seeds in the same order)
+    checked, mismatched = recheck_proofs(lanes, lanes[0])
     proofs = L if shard else L * world
     transforms = ("13 transforms (6 idft(n); 6 coset_dft and 1 coset_idft over the 6n quotient "
                   "domain, each as 3 coset blocks of 2n) + 11 MSMs")
@@ -653,11 +708,12 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
                         "the current GPU proof"
                         + (f"; {L} proofs in flight per GPU (plk_prover lanes sharing one key "
                            "and SRS)" if L > 1 else "")
-                        + (f"; every commit split over {world} GPUs by SRS slice (RCCL "
-                           "all-gather of partial points + host fold), NTT / elementwise "
+                        + (f"; every commit split over {world} GPU(s) by SRS slice "
+                           f"({transport(dist)} all-gather of partial points + host fold), NTT / elementwise "
                            "rounds replicated on every GPU" if shard else ""),
             "n": n, "log_n": k, "proofs_per_step": proofs,
-            "parallelism": (f"msm-shard x{world} x {L} lane(s)" if shard else
+            "parallelism": (f"msm-shard x{world} x {L} lane(s), partials all-gathered over "
+                            f"{transport(dist)}" if shard else
                             f"proof-batch x{world * L} ({L} concurrent prover lane(s) per GPU)"),
             "msm_window_bits": cbits,
             "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
@@ -666,6 +722,15 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
             "synthesis_host_overlapped": 1e3 * sum(sum(ln.synth_s) for ln in lanes) / (steps * L),
             "prove_latency": 1e3 * sum(sum(ln.prove_s) for ln in lanes) / (steps * L),
         },
+        "proofs_checked": checked - len(mismatched),
+        "proofs_check": ("each lane's last timed proof re-proved alone on one lane after the "
+                         "timed region, byte-identical"),
+        "host_cores": {"needed_per_rank": need, "needed_node": need_node,
+                       "available_node": avail_node, "lanes_requested": len(lanes_all),
+                       "lanes_run": L,
+                       "note": "lanes x measured synthesis s / step s (warmup), summed over "
+                               "the node's ranks; lanes are lowered when the node would be "
+                               "oversubscribed"},
     }
     # roofline of the dominant kernel (k_accumulate, ~60 % of a proof's GPU time) from its
     # solo launches; the in-workload averages beside them
@@ -703,13 +768,21 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
                                                    gpu_value=result["value"])
     if rank == 0:
         print(json.dumps(result), flush=True)
-    for ln in lanes:
+    for ln in lanes_all:
         ln.pool.shutdown(wait=True)
         ln.lane.close()
     if exchange is not None:
         exchange.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
+    if mismatched:
+        raise SystemExit(f"bench.py: {len(mismatched)} of {checked} concurrent proofs differ "
+                         f"from the same proof made alone (seeds {mismatched})")
+
+
+def transport(dist) -> str:
+    """The process group's transport, as the line reports it."""
+    return "RCCL" if dist.get_backend() == "nccl" else "gloo (host memory)"
 
 
 def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
@@ -847,7 +920,7 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
             raise SystemExit("GPU result differs from the oracle")
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -889,16 +962,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.shard_msm:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:  # --shard-msm on one GPU, no launcher
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
         # one rank per GPU; ranks beyond the device count share GPUs (a gloo rehearsal of
         # the multi-rank path on a one-GPU box: RCCL refuses two ranks on one device)
         local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    rank=rank, world_size=world)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
         torch.cuda.set_device(0)
     device = torch.device("cuda", torch.cuda.current_device())
@@ -913,7 +992,9 @@ def main():
     torch.cuda.set_stream(stream)
     if args.mode in ("ntt", "msm"):
         return run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n)
-    shard = args.shard_msm and world > 1
+    # --shard-msm at world 1 runs the sharded path's whole exchange (communicator, device
+    # staging, the exchange thread) with one slice: the configs[4] form on one GPU
+    shard = args.shard_msm
     if args.mode == "prove":
         return run_full(args, plk, torch, dist, world, rank, device, k, n, shard)
     hp = HotPath(plk, torch, k, device, seed=1 if shard else 1000 * rank + 1, shard=shard)
@@ -972,7 +1053,7 @@ def main():
             "workload": f"create_proof hot path at n=2^{k}: 7 idft(n) + 4 dft(n) + 7 coset_dft(8n) "
                         f"+ 1 coset_idft(8n) + 11 KZG commits (MSM n, in the reference's 4 independent groups)",
             "n": n, "log_n": k, "hot_path_only": True, "proofs_per_step": 1 if shard else world,
-            "parallelism": (f"msm-shard x{world} (SRS slices, RCCL all-gather of partials)"
+            "parallelism": (f"msm-shard x{world} (SRS slices, {transport(dist)} all-gather of partials)"
                             if shard else f"proof-batch x{world} (one proof per GPU per step)"),
             "msm_window_bits": (hp.pp.local if shard else hp.pp).last_msm_stats()[2],
         },
@@ -980,13 +1061,19 @@ def main():
             "ntt_n_x11": t_ntt_n, "ntt_8n_x8": t_ntt_8n, "msm_accumulate_4_batches": t_acc,
             "other": ms_per_step - t_ntt_n - t_ntt_8n - t_acc,
         },
-        "roofline": {
-            "bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": launch_ms,
-            "note": "integer-VALU-bound path (no MFMA); HBM reported as the required secondary roofline",
-        },
     }
+    if kname == "k_ntt_pass":  # the binding (Fr-multiply issue) roofline at top level
+        k8 = k + 3
+        muls = (8 * n / 2) * k8 / (launch_ms * 1e-3)
+        result["roofline"] = {
+            "bound": "valu", "kernel": "k_ntt_pass (all passes of one 8n coset transform)",
+            "achieved": muls, "peak": FR_MUL_PEAK, "unit": "Fr mul/s", "frac": muls / FR_MUL_PEAK,
+            "peak_source": "measured by tools/ubench_limbs.hip (ffr.hpp Fr multiply, whole chip)",
+            "ops": "(N/2) log2 N butterfly multiplications per transform, N = 8n",
+            "traffic": traffic, "avg_launch_ms": launch_ms,
+            "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes},
+            "note": "integer-VALU-bound path (no MFMA); HBM is the secondary roofline"}
     if kname == "k_accumulate" and acc:  # the binding (VALU issue) roofline at top level
         adds = sum(hp.msm_adds) / len(hp.msm_adds)
         roof = binding_roofline(valu_roofline(adds / (launch_ms * 1e-3)), achieved, alg_bytes,
@@ -999,7 +1086,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(k, hp.pp, cpu_threads(args))
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -195,6 +195,36 @@ int plk_ntt(plk_domain* d, plk_fr* inout, size_t len_in, int dir, int coset) {
   PLK_API_END
 }
 
+// plk_ntt with the caller's stream (SURVEY §8b's signature): stream-ordered staging buffer
+// and scratch of its own (hipMallocAsync), so calls on different streams of one domain do not
+// share the domain's io / scratch buffers; returns once `inout` holds the result.
+int plk_ntt_stream(plk_domain* d, plk_fr* inout, size_t len_in, int dir, int coset,
+                   void* stream) {
+  PLK_API_BEGIN
+  if (!d || !inout || (dir != 1 && dir != -1) || len_in > d->n) return PLK_E_ARG;
+  DeviceGuard g(d->ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : d->ctx->stream;
+  void* buf = nullptr;  // n elements of data + 2n of scratch
+  if (hipMallocAsync(&buf, 3 * d->n * sizeof(Fr), s) != hipSuccess) return PLK_E_OOM;
+  Fr* io = static_cast<Fr*>(buf);
+  int st = PLK_OK;
+  hipError_t e = hipSuccess;
+  if (len_in) e = hipMemcpyAsync(io, inout, len_in * sizeof(Fr), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    st = ntt_run(d, io, io, len_in, dir, coset, io + d->n, s, 1);
+    if (st == PLK_OK)
+      e = hipMemcpyAsync(inout, io, d->n * sizeof(Fr), hipMemcpyDeviceToHost, s);
+  }
+  (void)hipFreeAsync(buf, s);
+  if (e == hipSuccess && st == PLK_OK) e = stream_wait(s);
+  if (e != hipSuccess) {
+    last_hip_error() = e;
+    return PLK_E_DEVICE;
+  }
+  return st;
+  PLK_API_END
+}
+
 int plk_ntt_dev(plk_domain* d, const plk_fr* d_in, plk_fr* d_out, size_t len_in, int dir,
                 int coset, plk_fr* d_scratch, void* stream) {
   PLK_API_BEGIN

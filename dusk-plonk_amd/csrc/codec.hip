@@ -11,8 +11,8 @@
 // prover builds it (linearization_poly.rs:117-134), the order of plk_proof. SCALE's Decode
 // of a bool rejects bytes other than 0 and 1; this decoder also rejects limbs that are not
 // canonical and finite points off y^2 = x^3 + 4 (the curve check the verifier relies on).
-// The identity is encoded (x = 0, y = 0, is_infinity = 1); on decode any canonical
-// coordinates under the flag mean the identity (zkcrypto crates write y = one).
+// The identity is encoded (x = 0, y = 0, is_infinity = 1); decode accepts that and the
+// zkcrypto form (x = 0, y = one, is_infinity = 1) and rejects other coordinates under the flag.
 // Host code only.
 #include <cstring>
 
@@ -42,6 +42,19 @@ bool canonical(const uint64_t* l) {
     if (w != C::P[i]) return w < C::P[i];
   }
   return false;  // equal to the modulus
+}
+
+bool is_zero6(const uint64_t* l) {
+  for (int i = 0; i < 6; ++i)
+    if (l[i]) return false;
+  return true;
+}
+// Montgomery one of Fp (R mod p), as LE u64 limbs
+bool is_fp_one(const uint64_t* l) {
+  const Fp one = fe_one<FpCfg>();
+  for (int i = 0; i < 6; ++i)
+    if (l[i] != ((uint64_t)one.v[2 * i] | ((uint64_t)one.v[2 * i + 1] << 32))) return false;
+  return true;
 }
 
 template <class C>
@@ -115,9 +128,10 @@ int plk_proof_decode(const uint8_t* in, size_t len, plk_proof* proof) {
     g->infinity = q[96];
     if (!canonical<FpCfg>(g->x) || !canonical<FpCfg>(g->y)) return PLK_E_ARG;
     if (g->infinity) {
-      // the flag alone marks the identity: zkcrypto-style crates write (0, one, true), this
-      // encoder (0, 0, true); a derived Decode keeps whatever coordinates came, so any
-      // canonical pair is accepted and normalised to this ABI's (0, 0, 1)
+      // the identity's two known encodings: (0, 0, true) (this encoder) and (0, one, true)
+      // (zkcrypto-style crates); any other coordinates under the flag are rejected, so
+      // decode stays injective up to these two. Normalised to this ABI's (0, 0, 1).
+      if (!is_zero6(g->x) || !(is_zero6(g->y) || is_fp_one(g->y))) return PLK_E_ARG;
       std::memset(g->x, 0, sizeof g->x);
       std::memset(g->y, 0, sizeof g->y);
     } else if (!on_curve(*g)) {

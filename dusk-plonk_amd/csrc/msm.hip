@@ -134,9 +134,11 @@ __global__ void k_block_scan(uint32_t* __restrict__ blockhist, uint32_t nblk, ui
                              uint32_t* __restrict__ counts, uint32_t* __restrict__ zero_a,
                              uint32_t* __restrict__ zero_b) {
   const uint32_t slot = blockIdx.y;
-  if (blockIdx.x == 0 && zero_a && threadIdx.x < kChunkMax) {
-    zero_a[(size_t)slot * kChunkMax + threadIdx.x] = 0;
-    zero_b[(size_t)slot * kChunkMax + threadIdx.x] = 0;
+  if (blockIdx.x == 0 && zero_a) {  // a loop: kChunkMax (PLK_CHUNK_MAX) may exceed the block
+    for (uint32_t l = threadIdx.x; l < (uint32_t)kChunkMax; l += blockDim.x) {
+      zero_a[(size_t)slot * kChunkMax + l] = 0;
+      zero_b[(size_t)slot * kChunkMax + l] = 0;
+    }
   }
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;

@@ -107,10 +107,20 @@ class ExchangeService:
     path), so each awaited request arrives: lanes never wait on anything but their own
     exchange. `close()` (every rank, after its lanes stopped) ends the thread: rank 0
     broadcasts a stop entry once nothing is pending.
+
+    Failure: a lane whose proof fails BEFORE an exchange (a host error on one rank only) must
+    still reach that exchange with an error status — the C++ prover sends its status in the
+    exchanged words — or the peers wait for it (REQUEST_TIMEOUT_S). If the exchange thread
+    itself fails, it wakes this rank's lanes with the error and destroys the service group, so
+    the peers' pending collectives fail rather than block (the group is created with a
+    GROUP_TIMEOUT_S timeout for backends that only time out).
     """
 
     MAX_BATCH = 64  # lanes served by one all-gather
     REQUEST_TIMEOUT_S = 600.0  # a lane rank 0 scheduled must reach its exchange by then
+    # the service group's collective timeout: a peer whose exchange thread failed (and tore
+    # its group down) makes this rank's pending collective fail instead of waiting forever
+    GROUP_TIMEOUT_S = 900.0
 
     def __init__(self, group=None, device=None):
         """Collective: every rank of `group` (default: the world) constructs it at the same
@@ -122,7 +132,9 @@ class ExchangeService:
 
         self.torch, self.dist = torch, dist
         ranks = dist.get_process_group_ranks(group) if group is not None else None
-        self.group = dist.new_group(ranks=ranks, backend=dist.get_backend(group))
+        import datetime
+        self.group = dist.new_group(ranks=ranks, backend=dist.get_backend(group),
+                                    timeout=datetime.timedelta(seconds=self.GROUP_TIMEOUT_S))
         self.device = device
         self.world = dist.get_world_size(self.group)
         self.rank = dist.get_rank(self.group)
@@ -246,6 +258,12 @@ class ExchangeService:
                         r.done.set()
                     dq.clear()
                 self.cv.notify_all()
+            # peers may be blocked in this group's next collective: tear the group down so
+            # theirs fails (or times out after GROUP_TIMEOUT_S) instead of waiting forever
+            try:
+                dist.destroy_process_group(self.group)
+            except Exception:  # noqa: BLE001 — already torn down / backend refused
+                pass
 
     def close(self, timeout: float | None = 120.0):
         """Stop the exchange thread (call on every rank once its lanes are done)."""

@@ -41,7 +41,8 @@ ABI_SYMBOLS = (
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
     "plk_srs_last_msm_stats", "plk_debug_field_op", "plk_commit_batch_dev",
     "plk_srs_setup_range", "plk_g1_sum", "plk_msm_sharded", "plk_srs_msm_stats_reset",
-    "plk_srs_cum_msm_stats",
+    "plk_srs_cum_msm_stats", "plk_ntt_stream", "plk_aggregate_witness",
+    "plk_aggregate_witness_dev",
     # prover (dusk-plonk_amd/prover.py binds these)
     "plk_composer_create", "plk_composer_destroy", "plk_composer_size",
     "plk_composer_append_witness", "plk_composer_witness_value", "plk_composer_set_witness",
@@ -97,6 +98,9 @@ def _lib():
             "plk_domain_vanishing_over_coset": (i32, [vp, u64, vp]),
             "plk_ntt": (i32, [vp, vp, sz, i32, i32]),
             "plk_ntt_dev": (i32, [vp, vp, vp, sz, i32, i32, vp, vp]),
+            "plk_ntt_stream": (i32, [vp, vp, sz, i32, i32, vp]),
+            "plk_aggregate_witness": (i32, [vp, vp, vp, sz, vp, vp, vp, C.POINTER(sz)]),
+            "plk_aggregate_witness_dev": (i32, [vp, vp, vp, sz, vp, vp, vp, C.POINTER(sz), vp]),
             "plk_ntt_batch_dev": (i32, [vp, vp, sz, i32, i32, vp]),
             "plk_srs_setup": (i32, [vp, vp, sz, vp, pp]),
             "plk_srs_load": (i32, [vp, vp, sz, pp]),
@@ -277,26 +281,32 @@ class Fft:
         return PointsValue(out)
 
     # -- transforms
-    def _run(self, vals: np.ndarray, direction: int, coset: int) -> np.ndarray:
+    def _run(self, vals: np.ndarray, direction: int, coset: int, stream: int = 0) -> np.ndarray:
+        """stream != 0: plk_ntt_stream on that hipStream_t (own staging, so threads with
+        their own streams may share this Fft); else plk_ntt on the context's stream."""
         vals = _as_fr_array(vals)
         if vals.shape[0] > self._n:
             raise ValueError(f"input of length {vals.shape[0]} exceeds the domain size {self._n}")
         buf = np.zeros((self._n, 4), dtype=np.uint64)
         buf[: vals.shape[0]] = vals
-        _check(_lib().plk_ntt(self._d, _ptr(buf), vals.shape[0], direction, coset), "plk_ntt")
+        if stream:
+            _check(_lib().plk_ntt_stream(self._d, _ptr(buf), vals.shape[0], direction, coset,
+                                         C.c_void_p(stream)), "plk_ntt_stream")
+        else:
+            _check(_lib().plk_ntt(self._d, _ptr(buf), vals.shape[0], direction, coset), "plk_ntt")
         return buf
 
-    def dft(self, coeffs: Coefficients) -> PointsValue:
-        return PointsValue(self._run(coeffs.values, 1, 0))
+    def dft(self, coeffs: Coefficients, stream: int = 0) -> PointsValue:
+        return PointsValue(self._run(coeffs.values, 1, 0, stream))
 
-    def idft(self, points: PointsValue) -> Coefficients:
-        return Coefficients(self._run(points.values, -1, 0))
+    def idft(self, points: PointsValue, stream: int = 0) -> Coefficients:
+        return Coefficients(self._run(points.values, -1, 0, stream))
 
-    def coset_dft(self, coeffs: Coefficients) -> PointsValue:
-        return PointsValue(self._run(coeffs.values, 1, 1))
+    def coset_dft(self, coeffs: Coefficients, stream: int = 0) -> PointsValue:
+        return PointsValue(self._run(coeffs.values, 1, 1, stream))
 
-    def coset_idft(self, points: PointsValue) -> Coefficients:
-        return Coefficients(self._run(points.values, -1, 1))
+    def coset_idft(self, points: PointsValue, stream: int = 0) -> Coefficients:
+        return Coefficients(self._run(points.values, -1, 1, stream))
 
     # -- device-resident variants (torch tensors of dtype int64, shape [n, 4], on cuda)
     def ntt_dev(self, d_in_ptr: int, d_out_ptr: int, len_in: int, direction: int, coset: bool,
@@ -431,6 +441,37 @@ class PlonkParams:
             raise PlonkError(st, "commit_batch_dev")
         return [Commitment(outs[i]) if sts[i] == PLK_OK else PlonkError(sts[i], "commit")
                 for i in range(k)]
+
+    def compute_aggregate_witness(self, polys, point, challenge) -> Coefficients:
+        """PlonkParams::compute_aggregate_witness (prover.rs:422-450):
+        (sum_i challenge^i polys[i]) / (X - point), remainder dropped (plk_aggregate_witness)."""
+        arrs = [_as_fr_array(p.values if isinstance(p, Coefficients) else p) for p in polys]
+        k = len(arrs)
+        ptrs = (C.c_void_p * max(k, 1))(*[C.c_void_p(a.ctypes.data) for a in arrs])
+        lens = (C.c_size_t * max(k, 1))(*[a.shape[0] for a in arrs])
+        pt = _as_fr_array(point).reshape(4)
+        ch = _as_fr_array(challenge).reshape(4)
+        m = max((a.shape[0] for a in arrs), default=0)
+        out = np.zeros((max(m - 1, 1), 4), dtype=np.uint64)
+        n_out = C.c_size_t()
+        _check(_lib().plk_aggregate_witness(self.ctx.handle, ptrs, lens, k, _ptr(pt), _ptr(ch),
+                                            _ptr(out), C.byref(n_out)), "compute_aggregate_witness")
+        return Coefficients(out[: n_out.value])
+
+    def compute_aggregate_witness_dev(self, ptrs_lens, point, challenge, d_out: int,
+                                      stream: int = 0) -> int:
+        """Device form (plk_aggregate_witness_dev): [(ptr, len)] -> d_out; returns its length."""
+        k = len(ptrs_lens)
+        ptrs = (C.c_void_p * max(k, 1))(*[C.c_void_p(p) for p, _ in ptrs_lens])
+        lens = (C.c_size_t * max(k, 1))(*[n for _, n in ptrs_lens])
+        pt = _as_fr_array(point).reshape(4)
+        ch = _as_fr_array(challenge).reshape(4)
+        n_out = C.c_size_t()
+        _check(_lib().plk_aggregate_witness_dev(self.ctx.handle, ptrs, lens, k, _ptr(pt), _ptr(ch),
+                                                C.c_void_p(d_out or None), C.byref(n_out),
+                                                C.c_void_p(stream or None)),
+               "compute_aggregate_witness_dev")
+        return n_out.value
 
     def msm_stats_reset(self):
         _check(_lib().plk_srs_msm_stats_reset(self._h), "plk_srs_msm_stats_reset")

@@ -88,6 +88,11 @@ int plk_domain_vanishing_over_coset(const plk_domain* d, uint64_t poly_degree, p
  *            key.rs:121-131)
  * `inout` must hold n elements; natural order in and out. */
 int plk_ntt(plk_domain* d, plk_fr* inout, size_t len_in, int dir, int coset);
+/* plk_ntt on the caller's stream (hipStream_t as void*, NULL = the context's stream), the
+ * signature of SURVEY §8b: same semantics, host buffer in and out, returns once `inout`
+ * holds the result (the reference's Fft calls block). Staging and scratch are stream-ordered
+ * allocations of its own, so callers on different streams may share one domain. */
+int plk_ntt_stream(plk_domain* d, plk_fr* inout, size_t len_in, int dir, int coset, void* stream);
 /* Device-pointer variant: d_in -> d_out (may alias; both hold n elements). d_scratch is
  * NULL (use the domain's scratch — then calls on one domain must share one stream) or a
  * device buffer of 2*n elements owned by the caller. */
@@ -132,6 +137,20 @@ int plk_commit_dev(plk_srs* srs, const plk_fr* d_coeffs, size_t len, plk_g1* out
  * statuses (nullable) gets each commit's status; returns PLK_E_DEGREE if any failed. */
 int plk_commit_batch_dev(plk_srs* srs, const plk_fr* const* d_coeffs, const size_t* lens,
                          size_t count, plk_g1* outs, int* statuses, void* stream);
+
+/* PlonkParams::compute_aggregate_witness(&[p_0..p_(k-1)], &point, &v) (prover.rs:422-438,
+ * 444-450): W(X) = (sum_i v^i p_i(X)) / (X - point), the remainder dropped (Ruffini). The
+ * k polynomials (d_polys[i], lens[i] coefficients) are device pointers; d_out receives
+ * *out_len = max(lens) - 1 coefficients (0 when every polynomial is constant or empty),
+ * stream-ordered. point and v must be canonical (PLK_E_ARG otherwise). The same division
+ * plk_prove runs for its two openings; exported so the primitive itself can be replaced. */
+int plk_aggregate_witness_dev(plk_ctx* ctx, const plk_fr* const* d_polys, const size_t* lens,
+                              size_t count, const plk_fr* point, const plk_fr* v,
+                              plk_fr* d_out, size_t* out_len, void* stream);
+/* Host-buffer variant on the context's stream; returns when `out` holds the result. */
+int plk_aggregate_witness(plk_ctx* ctx, const plk_fr* const* polys, const size_t* lens,
+                          size_t count, const plk_fr* point, const plk_fr* v, plk_fr* out,
+                          size_t* out_len);
 
 /* Host-side sum of n affine points (canonical affine out): the local fold after the RCCL
  * all-gather of per-GPU partial commitments of a sharded MSM. Needs no GPU. */
@@ -287,7 +306,8 @@ int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int ra
  * PLK_PROOF_SCALE_BYTES. Decode rejects (PLK_E_ARG) a wrong length, a non-boolean flag,
  * limbs >= the modulus, and finite points not on y^2 = x^3 + 4. The identity (ASSUMED
  * encoding) is written as x = 0, y = 0, is_infinity = 1; decode takes is_infinity = 1 with
- * any canonical x, y (e.g. zkcrypto's y = one) as the identity and returns it as (0, 0, 1). */
+ * (x, y) = (0, 0) or zkcrypto's (0, one) as the identity and returns it as (0, 0, 1); other
+ * coordinates under the flag are rejected. */
 #define PLK_PROOF_SCALE_BYTES (11 * 97 + 16 * 32)
 int plk_proof_encode(const plk_proof* proof, uint8_t* out, size_t cap, size_t* len);
 int plk_proof_decode(const uint8_t* in, size_t len, plk_proof* proof);

@@ -258,6 +258,32 @@ def poly_eval(coeffs, x: int) -> int:
     return acc
 
 
+def ruffini(coeffs, z: int):
+    """Synthetic division by (X - z), remainder dropped (zksnarks' Coefficients::ruffini,
+    absent crate; called through compute_aggregate_witness): q_(i-1) = c_i + z q_i from the
+    top coefficient down. len(q) = len(c) - 1."""
+    q = [0] * max(len(coeffs) - 1, 0)
+    acc = 0
+    for i in range(len(coeffs) - 1, 0, -1):
+        acc = (coeffs[i] + z * acc) % R_MOD
+        q[i - 1] = acc
+    return q
+
+
+def aggregate_witness(polys, point: int, v: int):
+    """PlonkParams::compute_aggregate_witness(&[p_0..p_(k-1)], &point, &v)
+    (reference call sites src/prover.rs:422-438 and :444-450): the v-power combination
+    sum_i v^i p_i (powers 1, v, v^2, .. in slice order), then ruffini(point). Plain ints."""
+    m = max((len(p) for p in polys), default=0)
+    acc = [0] * m
+    vp = 1
+    for p in polys:
+        for j, c in enumerate(p):
+            acc[j] = (acc[j] + vp * c) % R_MOD
+        vp = vp * v % R_MOD
+    return ruffini(acc, point)
+
+
 # --------------------------------------------------------------------------- G1
 def _fp_inv(x):
     return pow(x, P_MOD - 2, P_MOD)

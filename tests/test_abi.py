@@ -39,6 +39,10 @@ def test_null_arguments_are_rejected_without_gpu(plk):
     assert lib.plk_commit(None, None, 0, None) == plk.PLK_E_ARG
     assert lib.plk_srs_len(None, None) == plk.PLK_E_ARG
     assert lib.plk_msm_sharded(None, 0, None, 0, None) == plk.PLK_E_ARG
+    assert lib.plk_ntt_stream(None, None, 0, 1, 0, None) == plk.PLK_E_ARG
+    assert lib.plk_aggregate_witness(None, None, None, 0, None, None, None, None) == plk.PLK_E_ARG
+    assert lib.plk_aggregate_witness_dev(None, None, None, 0, None, None, None, None,
+                                         None) == plk.PLK_E_ARG
     from dusk_plonk_amd.prover import _bind
     b = _bind()
     assert b.plk_prover_create(None, None) == plk.PLK_E_ARG

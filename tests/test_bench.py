@@ -119,3 +119,24 @@ def test_gpus_2_shard_msm_launches_ranks_itself():
     assert d["config"]["parallelism"].startswith("msm-shard x2")
     # all ranks prove the same proofs: value counts each once
     assert d["value"] == pytest.approx(4096 * 2 * 2 / (d["ms_per_step"] * 2e-3), rel=1e-6)
+
+
+@pytest.mark.gpu
+def test_prove_mode_checks_its_proofs():
+    """The prove line re-proves every lane's last timed proof alone and compares bytes."""
+    d = run_bench("--log-n", "12", "--steps", "2", "--warmup", "1", "--lanes", "3",
+                  "--no-cpu-baseline")
+    assert d["proofs_checked"] == 3
+    hc = d["host_cores"]
+    assert hc["lanes_run"] == 3 and hc["needed_per_rank"] > 0 and hc["available_node"] >= 1
+
+
+@pytest.mark.gpu
+def test_shard_msm_world1_over_rccl():
+    """`bench.py --shard-msm` at world 1 under nccl: the configs[4] form with its whole RCCL
+    exchange on the one GPU (no launcher), one line, transport named."""
+    d = run_bench("--shard-msm", "--log-n", "12", "--steps", "2", "--warmup", "1", "--lanes",
+                  "2", "--no-cpu-baseline", timeout=200)
+    check_contract(d, 2, 1)
+    assert d["scaling"] == "strong" and "RCCL" in d["config"]["parallelism"]
+    assert d["proofs_checked"] == 2

@@ -171,3 +171,27 @@ def test_c_oracle_ntt_roundtrip_mid(oracle):
         x = random_fr(1 << k, seed=k)
         assert np.array_equal(oracle.idft(oracle.dft(x, k), k), x)
         assert np.array_equal(oracle.coset_idft(oracle.coset_dft(x, k), k), x)
+
+
+def test_ruffini_restatement_divides():
+    """pyref.ruffini is exact division for p(X) - p(z): q(X)(X - z) + p(z) = p(X), and
+    aggregate_witness is ruffini of the v-power combination (prover.rs:422-450)."""
+    import random
+    import pyref as P
+    rng = random.Random(3)
+    for m in (0, 1, 2, 7, 40):
+        c = [rng.randrange(P.R_MOD) for _ in range(m)]
+        z = rng.randrange(P.R_MOD)
+        q = P.ruffini(c, z)
+        assert len(q) == max(m - 1, 0)
+        x = rng.randrange(P.R_MOD)
+        if m:
+            lhs = (P.poly_eval(q, x) * (x - z) + P.poly_eval(c, z)) % P.R_MOD
+            assert lhs == P.poly_eval(c, x)
+    polys = [[rng.randrange(P.R_MOD) for _ in range(k)] for k in (5, 9, 3)]
+    v, z = rng.randrange(P.R_MOD), rng.randrange(P.R_MOD)
+    comb = [0] * 9
+    for i, p in enumerate(polys):
+        for j, cc in enumerate(p):
+            comb[j] = (comb[j] + pow(v, i, P.R_MOD) * cc) % P.R_MOD
+    assert P.aggregate_witness(polys, z, v) == P.ruffini(comb, z)

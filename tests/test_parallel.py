@@ -482,3 +482,84 @@ def _sharded_2_20_worker(rank, world, port, q):
 def test_sharded_prover_2_20_equals_fixture(plk, gpu_ctx):
     out = _spawn(_sharded_2_20_worker, 2)
     assert out == {0: True, 1: True}
+
+
+def _rccl_world1_worker(rank, world, port, q, logn, lanes):
+    """The RCCL data path of the sharded prover on the one GPU: torch.distributed over
+    `nccl` (RCCL) at world size 1 on cuda:0. Exercises what the gloo rehearsals cannot:
+    communicator init on the exchange thread, its torch.cuda.Stream, device staging of the
+    payloads and `.cpu()` syncs while other lanes' kernels hold the CUs; plus the device
+    forms of torch_allgather and gather_fold (ShardedPlonkParams). Every sharded proof must
+    equal plk_prove's bytes (reference commit groups: prover.rs:133-136,194,262-265,440,452)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import threading
+    import torch
+    import torch.distributed as dist
+    from oracle_lib import random_fr
+    import dusk_plonk_amd as plk
+    from dusk_plonk_amd.parallel import (ExchangeService, ShardedPlonkParams, shard_prover_lane,
+                                         srs_slice, torch_allgather)
+    from dusk_plonk_amd.prover import Plonk, PlonkKey
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        ok = dist.get_backend() == "nccl"
+        ag = torch_allgather(None, dev)  # the byte all-gather's device path
+        ok &= ag(b"\x01\x02\x03") == b"\x01\x02\x03"
+        tau = random_fr(1, seed=71)[0]
+        ctx = plk.Context.default(0)
+        n = 1 << logn
+        pp = plk.PlonkParams.setup(logn, tau, ctx)
+        # the sharded single MSM with its partials gathered from HBM
+        spp = ShardedPlonkParams(logn, tau, ctx=ctx)
+        coef = torch.from_numpy(random_fr(n, 9).view(np.int64)).to(dev)
+        s = torch.cuda.current_stream().cuda_stream
+        got = spp.commit_dev(coef.data_ptr(), n, s, dev)
+        want = pp.commit_dev(coef.data_ptr(), n, s)
+        ok &= np.array_equal(got.words, want.words)
+
+        def circ(seed):
+            cs = Plonk()
+            cs.synthetic_chain(n - 15, seed)
+            cs.append_public(seed + 7)
+            return cs
+        prover, _ = PlonkKey.compile_composer(pp, b"rccl", circ(1))
+        seeds = list(range(5, 5 + 2 * lanes))
+        want = {s_: prover.prove_composer(circ(s_ + 10), s_)[0].raw_bytes() for s_ in seeds}
+        lns = [prover.lane() for _ in range(lanes)]
+        svc = ExchangeService(None, dev)
+        sl = srs_slice(tau, pp.n, world, rank, ctx)
+        for i, ln in enumerate(lns):
+            shard_prover_lane(ln, tau, pp.n, device=dev, slice_=sl, exchange=svc, lane_id=i)
+        results, errors = {}, []
+
+        def drive(i):
+            try:
+                for s_ in seeds[i::lanes]:
+                    results[s_] = lns[i].prove_composer(circ(s_ + 10), s_)[0].raw_bytes()
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+        ts = [threading.Thread(target=drive, args=(i,)) for i in range(lanes)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(300)
+        svc.close()
+        ok &= not errors and all(results.get(s_) == want[s_] for s_ in seeds)
+        ok &= svc.requests == 4 * len(seeds)  # 4 commit groups per proof
+        for ln in lns:
+            ln.close()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_prover_rccl_world1(plk, gpu_ctx):
+    """3 lanes sharded over an RCCL world of one (the device-tensor exchange runs for real)."""
+    out = _spawn(_rccl_world1_worker, 1, 14, 3)
+    assert out == {0: True}

@@ -60,9 +60,9 @@ def test_identity_commitment_round_trip(plk, fixture):
 FP = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 
 
-def test_identity_any_coordinates(plk, fixture):
-    """The flag alone marks the identity: zkcrypto-style (0, one, true) with one = 2^384 mod p
-    in Montgomery limbs decodes as the identity, normalised to (0, 0, 1)."""
+def test_identity_zkcrypto_encoding(plk, fixture):
+    """The identity's second known encoding: zkcrypto-style (0, one, true) with one = 2^384
+    mod p in Montgomery limbs decodes as the identity, normalised to (0, 0, 1)."""
     from dusk_plonk_amd.prover import Proof
     b = bytearray(fixture["scale"].tobytes())
     off = 4 * 97  # z_comm
@@ -77,7 +77,8 @@ def test_identity_any_coordinates(plk, fixture):
 
 
 @pytest.mark.parametrize("case", ["short", "long", "bool", "x_noncanonical", "off_curve",
-                                  "identity_noncanonical", "eval_noncanonical"])
+                                  "identity_noncanonical", "identity_other_coords",
+                                  "eval_noncanonical"])
 def test_decode_rejects(plk, fixture, case):
     from dusk_plonk_amd.prover import Proof
     b = bytearray(fixture["scale"].tobytes())
@@ -94,6 +95,8 @@ def test_decode_rejects(plk, fixture, case):
     elif case == "identity_noncanonical":
         b[96] = 1
         b[40:48] = (0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")
+    elif case == "identity_other_coords":  # canonical, but neither (0, 0) nor (0, one)
+        b[96] = 1
     elif case == "eval_noncanonical":
         off = 11 * 97
         b[off + 24: off + 32] = (0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")

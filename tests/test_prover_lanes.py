@@ -101,3 +101,55 @@ def test_gpu_proof_scale_round_trip(plk):
     q = Proof.from_bytes(data)
     assert q == p
     verify(vd, q, pi, tau)
+
+
+def test_twelve_lanes_2_20_concurrent_byte_exact(plk):
+    """The credited bench configuration byte-checked: ONE key at n = 2^20 (the fixture's
+    circuit and tau) and 12 prover lanes proving concurrently on the wide-bucket MSM path
+    (c = 20), 2 proofs each. Lane 0's first proof is the fixture's (circuit, blinding seed 7)
+    and must equal tests/golden/proof_2_20.npz (the restated CPU prover's bytes); every other
+    proof must equal the same (circuit, seed) proved afterwards on one lane alone. A race in
+    the shared window table, the per-lane workspaces or the readback generation stamps would
+    show here (reference: `Prover: Clone`, concurrent create_proof(&self), prover.rs:67-474)."""
+    import sys
+    from pathlib import Path
+    gold = Path(__file__).resolve().parent / "golden"
+    sys.path.insert(0, str(gold))
+    from make_proof_2_20 import BLIND_SEED, LABEL, LOG_N, TAU_SEED, circuit
+    from dusk_plonk_amd.prover import PlonkKey
+    from test_prover_oracle import bench_chain, build, tau_for
+    g = dict(np.load(gold / "proof_2_20.npz", allow_pickle=False))
+    tau_limbs, _ = tau_for(TAU_SEED)
+    pp = plk.PlonkParams.setup(LOG_N, tau_limbs)
+    prover, vd = PlonkKey.compile_composer(pp, LABEL, circuit())
+    assert np.array_equal(vd.comms, g["vk"])
+    L, per = 12, 2
+    lanes = [prover.lane() for _ in range(L)]
+    chain = (1 << LOG_N) - 15
+    jobs = {i: [(200 + i * per + j, 300 + i * per + j) for j in range(per)] for i in range(L)}
+    jobs[0][0] = (None, BLIND_SEED)  # the fixture's circuit (chain seed 77) and blinding
+
+    def circ(cseed):
+        return circuit() if cseed is None else build(bench_chain(chain, cseed))
+
+    def run(i):
+        out = {}
+        for cseed, bseed in jobs[i]:
+            cs = circ(cseed)
+            out[(cseed, bseed)] = lanes[i].prove_composer(cs, bseed)[0]
+        return out
+
+    got = {}
+    with cf.ThreadPoolExecutor(L) as ex:  # twelve lanes proving at the same time
+        for d in ex.map(run, range(L)):
+            got.update(d)
+    assert len(got) == L * per
+    assert got[(None, BLIND_SEED)].to_bytes() == g["scale"].tobytes()
+    alone = lanes[1]
+    for (cseed, bseed), p in got.items():
+        if cseed is None:
+            continue
+        want = alone.prove_composer(circ(cseed), bseed)[0]
+        assert p.raw_bytes() == want.raw_bytes(), (cseed, bseed)
+    for ln in lanes:
+        ln.close()
