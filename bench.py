@@ -66,6 +66,9 @@ def compiled_loop(kernel: str = "k_accumulateILb0E") -> dict:
             lib = os.environ.get("PLK_LIB") or str(ROOT / "dusk-plonk_amd" / "libplk.so")
             r = isa_count.largest_block(Path(lib), kernel)
             _ISA[kernel] = ({"v_mad_u64_u32": r["v_mad_u64_u32"], "instructions": r["instructions"],
+                             "valu_instructions": sum(n for op, n in r["mix"].items()
+                                                      if op.startswith("v_")),
+                             "s_nop": r["mix"].get("s_nop", 0),
                              "valu_cycles": isa_count.valu_cycles(r["mix"]),
                              "source": "compiled loop body (tools/isa_count.py on libplk.so)"}
                             if r else None)
@@ -532,7 +535,9 @@ def valu_roofline(adds_per_s):
                            "costs measured by tools/ubench_issue.hip (profiles/r03_ubench_issue.txt)",
             "valu_cycles_per_wave_of_adds": isa["valu_cycles"],
             "mads_per_point_add": isa["v_mad_u64_u32"],
-            "instructions_per_point_add": isa["instructions"], "mads_source": isa["source"],
+            "instructions_per_point_add": isa["instructions"],
+            "valu_instructions_per_point_add": isa.get("valu_instructions"),
+            "s_nop_per_point_add": isa.get("s_nop"), "mads_source": isa["source"],
             "mad": {"achieved": mads, "peak": VALU_MAD_PEAK, "unit": "mad/s",
                     "frac": mads / VALU_MAD_PEAK, "peak_source": VALU_MAD_PEAK_SOURCE}}
 
@@ -547,6 +552,8 @@ def binding_roofline(valu: dict, hbm_achieved_gbs: float, alg_bytes: float, traf
             "valu_cycles_per_wave_of_adds": valu["valu_cycles_per_wave_of_adds"],
             "mads_per_point_add": valu["mads_per_point_add"],
             "instructions_per_point_add": valu["instructions_per_point_add"],
+            "valu_instructions_per_point_add": valu.get("valu_instructions_per_point_add"),
+            "s_nop_per_point_add": valu.get("s_nop_per_point_add"),
             "mads_source": valu["mads_source"], "mad": valu["mad"], "traffic": traffic,
             "hbm": {"achieved": hbm_achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm_achieved_gbs / HBM_PEAK_GBS,

@@ -22,6 +22,7 @@
 // 2^-(B*L - 32N).
 #pragma once
 #include <type_traits>
+#include <utility>
 
 #include "ff.hpp"
 
@@ -168,6 +169,20 @@ struct RxMultipleK {
 
 #define PLK_RX __device__ __forceinline__
 
+#ifndef PLK_RX_PIN
+#define PLK_RX_PIN 0
+#endif
+// acc += x * y as ONE v_mad_u64_u32 on the running column accumulator. With PLK_RX_PIN the
+// accumulator passes an empty asm after each step, so LLVM cannot reassociate a column's
+// additions (it otherwise sums a column's products into a fresh accumulator and adds the
+// carried one with a 64-bit v_lshl_add_u64 per column).
+PLK_RX void rx_madd(uint64_t& acc, uint32_t x, uint32_t y) {
+  acc += (uint64_t)x * y;
+#if PLK_RX_PIN
+  __asm__("" : "+v"(acc));
+#endif
+}
+
 // Close column k of a split-capable product: acc holds the products (+ the incoming
 // carry), s2 the reduction terms and s3 a second product set (split columns only; both 0
 // otherwise). Below L the column's Montgomery digit m[k] is formed and its m_k p_0 added;
@@ -181,7 +196,7 @@ PLK_RX void rx_column_close(bool split, int k, uint64_t& acc, uint64_t s2, uint6
   if (!split) {
     if (k < L) {
       m[k] = ((uint32_t)acc * K.inv) & MASK;
-      acc += (uint64_t)m[k] * K.p[0];
+      rx_madd(acc, m[k], K.p[0]);
     } else {
       r.v[k - L] = (uint32_t)acc & MASK;
     }
@@ -254,10 +269,10 @@ PLK_RX Rx<C> rx_mul(const Rx<C>& a, const Rx<C>& b) {
       const int i0 = k < L ? 0 : k - L + 1, i1 = k < L ? k : L - 1;
       uint64_t s2 = 0;
 #pragma unroll
-      for (int i = i0; i <= i1; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+      for (int i = i0; i <= i1; ++i) rx_madd(acc, a.v[i], b.v[k - i]);
 #pragma unroll
       for (int i = i0; i <= i1; ++i)
-        if (i < k || k >= L) (PL.split[k] ? s2 : acc) += (uint64_t)m[i] * K.p[k - i];
+        if (i < k || k >= L) rx_madd(PL.split[k] ? s2 : acc, m[i], K.p[k - i]);
       rx_column_close<C>(PL.split[k], k, acc, s2, 0, m, r);
     }
   }
@@ -309,12 +324,12 @@ PLK_RX Rx<C> rx_mul_add(const Rx<C>& a, const Rx<C>& b, const Rx<C>& c, const Rx
       const int i0 = k < L ? 0 : k - L + 1, i1 = k < L ? k : L - 1;
       uint64_t s2 = 0, s3 = 0;
 #pragma unroll
-      for (int i = i0; i <= i1; ++i) acc += (uint64_t)a.v[i] * b.v[k - i];
+      for (int i = i0; i <= i1; ++i) rx_madd(acc, a.v[i], b.v[k - i]);
 #pragma unroll
-      for (int i = i0; i <= i1; ++i) (PL.split[k] ? s3 : acc) += (uint64_t)c.v[i] * d.v[k - i];
+      for (int i = i0; i <= i1; ++i) rx_madd(PL.split[k] ? s3 : acc, c.v[i], d.v[k - i]);
 #pragma unroll
       for (int i = i0; i <= i1; ++i)
-        if (i < k || k >= L) (PL.split[k] ? s2 : acc) += (uint64_t)m[i] * K.p[k - i];
+        if (i < k || k >= L) rx_madd(PL.split[k] ? s2 : acc, m[i], K.p[k - i]);
       rx_column_close<C>(PL.split[k], k, acc, s2, s3, m, r);
     }
   }
@@ -359,16 +374,211 @@ PLK_RX Rx<C> rx_sqr(const Rx<C>& a) {
       const int i0 = k < L ? 0 : k - L + 1, i1 = k < L ? k : L - 1;
       uint64_t s2 = 0;
 #pragma unroll
-      for (int i = i0; 2 * i < k; ++i) acc += (uint64_t)a.v[i] * a2[k - i];
-      if ((k & 1) == 0) acc += (uint64_t)a.v[k / 2] * a.v[k / 2];
+      for (int i = i0; 2 * i < k; ++i) rx_madd(acc, a.v[i], a2[k - i]);
+      if ((k & 1) == 0) rx_madd(acc, a.v[k / 2], a.v[k / 2]);
 #pragma unroll
       for (int i = i0; i <= i1; ++i)
-        if (i < k || k >= L) (PL.split[k] ? s2 : acc) += (uint64_t)m[i] * K.p[k - i];
+        if (i < k || k >= L) rx_madd(PL.split[k] ? s2 : acc, m[i], K.p[k - i]);
       rx_column_close<C>(PL.split[k], k, acc, s2, 0, m, r);
     }
   }
   r.v[L - 1] = (uint32_t)acc;
   return r;
+}
+
+// ---- interleaved product groups (split shapes: Fp 13 x 30) ----------------------------
+// NP independent Montgomery products computed column by column with their partial products
+// interleaved mad by mad: product p's column k is ONE chain on its own accumulator (the
+// incoming carry at the head, no second accumulator merged by a 64-bit add), and the chains
+// of the NP products alternate, so consecutive v_mad_u64_u32 never depend on each other (a
+// dependent pair needs a wait state on gfx950). Every step passes rx_pin so LLVM keeps each
+// chain as written instead of reassociating it (which is what costs the merge adds).
+// Kinds: kRxMul a*b, kRxSqr a^2 (b unused), kRxMulAdd a*b + c*d (one reduction, rx_mul_add's
+// bounds). Same results as rx_mul / rx_sqr / rx_mul_add, bit for bit.
+enum : int { kRxMul = 0, kRxSqr = 1, kRxMulAdd = 2 };
+
+PLK_RX void rx_pin(uint64_t& v) { __asm__ volatile("" : "+v"(v)); }
+
+template <class C, int NP>
+struct RxGroupState {
+  uint32_t m[NP][RxShape<C>::L], a2[NP][RxShape<C>::L];
+  uint64_t acc[NP];
+};
+
+// The mad order of column K: accumulator ids (3p: product p's acc, 3p + 1: its reduction
+// accumulator s2, 3p + 2: its second product set s3 — the last two in split columns only),
+// greedily taking the accumulator with the most terms left that differs from the previous
+// one, so no two consecutive mads share an accumulator whenever the counts allow it.
+template <int NP>
+struct RxColOrder {
+  int n = 0;
+  int acc[3 * 26 * 4] = {};  // at most 3 * 2L mads per product per column, L <= 13
+};
+
+template <class C, int K, int... KINDS>
+constexpr RxColOrder<sizeof...(KINDS)> rx_col_order() {
+  constexpr int L = RxShape<C>::L;
+  constexpr int NP = sizeof...(KINDS);
+  constexpr int kind[NP] = {KINDS...};
+  constexpr RxPlan<C, 1> P1{};
+  constexpr RxPlan<C, 2> P2{};
+  const int i0 = K < L ? 0 : K - L + 1, i1 = K < L ? K : L - 1;
+  const int n1 = i1 - i0 + 1;
+  const int ncross = (K + 1) / 2 - i0 > 0 ? (K + 1) / 2 - i0 : 0;
+  int nred = 0;
+  for (int i = i0; i <= i1; ++i)
+    if (i < K || K >= L) ++nred;
+  int left[3 * NP] = {};
+  for (int p = 0; p < NP; ++p) {
+    const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+    const int prod = kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? ncross + ((K & 1) == 0 ? 1 : 0) : 2 * n1;
+    if (!split) {
+      left[3 * p] = prod + nred;
+    } else {
+      left[3 * p] = kind[p] == kRxMulAdd ? n1 : prod;
+      left[3 * p + 1] = nred;
+      left[3 * p + 2] = kind[p] == kRxMulAdd ? n1 : 0;
+    }
+  }
+  RxColOrder<NP> o{};
+  int last = -1;
+  for (;;) {
+    int best = -1;
+    for (int q = 0; q < 3 * NP; ++q)
+      if (left[q] > 0 && q != last && (best < 0 || left[q] > left[best])) best = q;
+    if (best < 0) {  // only the previous accumulator has terms left
+      if (last >= 0 && left[last] > 0) best = last;
+      else break;
+    }
+    o.acc[o.n++] = best;
+    --left[best];
+    last = best;
+  }
+  return o;
+}
+
+// column K of every product of the group (K a template argument: every bound and branch
+// below is a compile-time constant). Each accumulator's terms are taken in a fixed order
+// (operand products first, then reduction terms); the interleaving is rx_col_order's.
+template <class C, int K, int... KINDS>
+PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* const* a,
+                            const Rx<C>* const* b, const Rx<C>* const* c, const Rx<C>* const* d,
+                            Rx<C>* const* out) {
+  constexpr int L = RxShape<C>::L;
+  constexpr int NP = sizeof...(KINDS);
+  constexpr int kind[NP] = {KINDS...};
+  constexpr RxConst<C> KC = RxK<C>::k;
+  constexpr RxPlan<C, 1> P1 = RxPlanK<C, 1>::k;
+  constexpr RxPlan<C, 2> P2 = RxPlanK<C, 2>::k;
+  constexpr int i0 = K < L ? 0 : K - L + 1, i1 = K < L ? K : L - 1;
+  constexpr int n1 = i1 - i0 + 1;                                      // terms of one a*b column
+  constexpr int ncross = (K + 1) / 2 - i0 > 0 ? (K + 1) / 2 - i0 : 0;  // a^2: i0 <= i, 2i < K
+  constexpr int nsq = ncross + ((K & 1) == 0 ? 1 : 0);
+  constexpr int rfirst = (K < L) ? 0 : i0;  // reduction terms: i in [rfirst, i1], i < K below L
+  constexpr int rlast = (K < L) ? K - 1 : i1;
+  constexpr RxColOrder<NP> ord = rx_col_order<C, K, KINDS...>();
+  uint64_t s2[NP], s3[NP];
+  int pos[3 * NP];  // next term of each accumulator
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    s2[p] = s3[p] = 0;
+    pos[3 * p] = pos[3 * p + 1] = pos[3 * p + 2] = 0;
+  }
+#pragma unroll
+  for (int e = 0; e < ord.n; ++e) {
+    const int q = ord.acc[e], p = q / 3, which = q % 3;
+    const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+    const int t = pos[q]++;
+    uint64_t& dst = which == 0 ? g.acc[p] : which == 1 ? s2[p] : s3[p];
+    // the accumulator's t-th term
+    const int nprod = which != 0 ? 0 : kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? nsq
+                                     : (split ? n1 : 2 * n1);
+    if (which == 2) {  // c*d of a split mul_add column
+      rx_madd(dst, c[p]->v[i0 + t], d[p]->v[K - i0 - t]);
+    } else if (which == 1 || t >= nprod) {  // a reduction term
+      const int i = rfirst + (which == 1 ? t : t - nprod);
+      rx_madd(dst, g.m[p][i], KC.p[K - i]);
+    } else if (kind[p] == kRxSqr) {
+      if (t < ncross) rx_madd(dst, a[p]->v[i0 + t], g.a2[p][K - i0 - t]);
+      else rx_madd(dst, a[p]->v[K / 2], a[p]->v[K / 2]);
+    } else if (t < n1) {
+      rx_madd(dst, a[p]->v[i0 + t], b[p]->v[K - i0 - t]);
+    } else {  // mul_add, non-split: c*d into acc
+      rx_madd(dst, c[p]->v[i0 + t - n1], d[p]->v[K - i0 - t + n1]);
+    }
+    rx_pin(dst);
+  }
+  (void)rlast;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+    rx_column_close<C>(split, K, g.acc[p], s2[p], s3[p], g.m[p], *out[p]);
+  }
+}
+
+template <class C, int... KINDS, int... KS>
+PLK_RX void rx_group_columns(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* const* a,
+                             const Rx<C>* const* b, const Rx<C>* const* c,
+                             const Rx<C>* const* d, Rx<C>* const* out,
+                             std::integer_sequence<int, KS...>) {
+  (rx_group_column<C, KS, KINDS...>(g, a, b, c, d, out), ...);
+}
+
+template <class C, int... KINDS>
+PLK_RX void rx_prod_group(const Rx<C>* const* a, const Rx<C>* const* b, const Rx<C>* const* c,
+                          const Rx<C>* const* d, Rx<C>* const* out) {
+  constexpr int L = RxShape<C>::L;
+  constexpr int NP = sizeof...(KINDS);
+  constexpr int kind[NP] = {KINDS...};
+  RxGroupState<C, NP> g;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    g.acc[p] = 0;
+    if (kind[p] == kRxSqr) {
+#pragma unroll
+      for (int i = 0; i < L; ++i) g.a2[p][i] = a[p]->v[i] << 1;
+    }
+  }
+  rx_group_columns<C, KINDS...>(g, a, b, c, d, out, std::make_integer_sequence<int, 2 * L - 1>{});
+#pragma unroll
+  for (int p = 0; p < NP; ++p) out[p]->v[L - 1] = (uint32_t)g.acc[p];
+}
+
+// the pair / triple forms used by the group law
+template <class C>
+PLK_RX void rx_mul2(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& a1, const Rx<C>& b1,
+                    Rx<C>& o0, Rx<C>& o1) {
+  const Rx<C>* a[2] = {&a0, &a1};
+  const Rx<C>* b[2] = {&b0, &b1};
+  Rx<C>* o[2] = {&o0, &o1};
+  rx_prod_group<C, kRxMul, kRxMul>(a, b, a, b, o);
+}
+template <class C>
+PLK_RX void rx_sqr2(const Rx<C>& a0, const Rx<C>& a1, Rx<C>& o0, Rx<C>& o1) {
+  const Rx<C>* a[2] = {&a0, &a1};
+  Rx<C>* o[2] = {&o0, &o1};
+  rx_prod_group<C, kRxSqr, kRxSqr>(a, a, a, a, o);
+}
+template <class C>
+PLK_RX void rx_mul3(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& a1, const Rx<C>& b1,
+                    const Rx<C>& a2, const Rx<C>& b2, Rx<C>& o0, Rx<C>& o1, Rx<C>& o2) {
+  const Rx<C>* a[3] = {&a0, &a1, &a2};
+  const Rx<C>* b[3] = {&b0, &b1, &b2};
+  Rx<C>* o[3] = {&o0, &o1, &o2};
+  rx_prod_group<C, kRxMul, kRxMul, kRxMul>(a, b, a, b, o);
+}
+// (a0 b0 + c0 d0, a1 b1, a2 b2): the fused Y3 beside ZZ3 and ZZZ3 (its 2 product sets
+// against their one each: the three accumulators alternate)
+template <class C>
+PLK_RX void rx_mul_add_mul2(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& c0, const Rx<C>& d0,
+                            const Rx<C>& a1, const Rx<C>& b1, const Rx<C>& a2, const Rx<C>& b2,
+                            Rx<C>& o0, Rx<C>& o1, Rx<C>& o2) {
+  const Rx<C>* a[3] = {&a0, &a1, &a2};
+  const Rx<C>* b[3] = {&b0, &b1, &b2};
+  const Rx<C>* c[3] = {&c0, &c0, &c0};
+  const Rx<C>* d[3] = {&d0, &d0, &d0};
+  Rx<C>* o[3] = {&o0, &o1, &o2};
+  rx_prod_group<C, kRxMulAdd, kRxMul, kRxMul>(a, b, c, d, o);
 }
 
 // a + b mod 2p-range: [0, 2p) + [0, 2p) -> [0, 2p)

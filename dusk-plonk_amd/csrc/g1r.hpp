@@ -132,7 +132,25 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
 //   * P == 0 (same x): ZZ3 = ZZ1 * P^2 == 0, and then X3 = R^2 + 6p, so R == 0 (same
 //     point: the sum is a doubling) <=> X3 == 0 mod p; otherwise the sum is infinity.
 // A zero ZZ3 is the single (rare) trigger; g1r_madd_lazy_fix finishes those cases.
+#ifndef PLK_MADD_GROUPED
+#define PLK_MADD_GROUPED 1
+#endif
 __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, const RFp& y2) {
+#if PLK_MADD_GROUPED
+  // the same nine reductions as independent groups whose chains interleave (ffr.hpp
+  // rx_prod_group): (U2, S2), (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3)
+  RFp U2, S2, PP, RR, PPP, Q;
+  rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
+  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
+  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
+  rx_sqr2(P, R, PP, RR);
+  G1R r;
+  rx_mul2(P, PP, p.X, PP, PPP, Q);
+  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
+  rx_mul_add_mul2(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP,
+                  p.ZZ, PP, p.ZZZ, PPP, r.Y, r.ZZ, r.ZZZ);
+  return r;
+#else
   const RFp U2 = rx_mul(x2, p.ZZ);
   const RFp S2 = rx_mul(y2, p.ZZZ);
   const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);  // (2p, 12p): U2 - X1 in (-8p, 2p)
@@ -149,6 +167,7 @@ __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, con
   r.ZZ = rx_mul(p.ZZ, PP);
   r.ZZZ = rx_mul(p.ZZZ, PPP);
   return r;
+#endif
 }
 
 // The result of p + (x2, y2) when g1r_madd_lazy_sl returned r with r.ZZ == 0; was_inf =
@@ -193,6 +212,22 @@ __device__ __forceinline__ G1R g1r_lazy_finish(const G1R& p) {
 // exceptional cases (either operand at infinity, equal x) all give ZZ3 = ZZ1 ZZ2 P^2 = 0 and
 // are repaired after, by g1r_add_lazy.
 __device__ __forceinline__ G1R g1r_add_lazy_sl(const G1R& p, const G1R& q) {
+#if PLK_MADD_GROUPED
+  // interleaved groups (ffr.hpp rx_prod_group): (U1, U2, ZZ1 ZZ2), (S1, S2, ZZZ1 ZZZ2),
+  // (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3)
+  RFp U1, U2, ZZ12, S1, S2, ZZZ12, PP, RR, PPP, Q;
+  rx_mul3(p.X, q.ZZ, q.X, p.ZZ, p.ZZ, q.ZZ, U1, U2, ZZ12);
+  const RFp P = rx_sub_u<FpCfg, 3>(U2, U1);  // U2 - U1 + 3p in (p, 5p)
+  rx_mul3(p.Y, q.ZZZ, q.Y, p.ZZZ, p.ZZZ, q.ZZZ, S1, S2, ZZZ12);
+  const RFp R = rx_sub_u<FpCfg, 3>(S2, S1);  // S2 - S1 + 3p in (p, 5p)
+  rx_sqr2(P, R, PP, RR);
+  rx_mul2(P, PP, U1, PP, PPP, Q);
+  G1R r;
+  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
+  rx_mul_add_mul2(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), S1), PPP,
+                  ZZ12, PP, ZZZ12, PPP, r.Y, r.ZZ, r.ZZZ);
+  return r;
+#else
   // ordered so that the operands die early: X1, X2 after P, Y1, Y2 after R, the Z's after
   // their products
   const RFp U1 = rx_mul(p.X, q.ZZ);
@@ -210,6 +245,7 @@ __device__ __forceinline__ G1R g1r_add_lazy_sl(const G1R& p, const G1R& q) {
   r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
   r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), S1), PPP);
   return r;
+#endif
 }
 
 // dbl-2008-s-1 on a lazy operand (X < 8p, Y < 4p, ZZ, ZZZ < 2p; normalised limbs) with the

@@ -401,7 +401,7 @@ int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
 int prover_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
                   const std::vector<size_t>& lens, plk_g1* outs, int* statuses,
                   size_t cap = SIZE_MAX) {
-  if (P->world > 1) return shard_commit(P, ptrs, lens, outs, statuses, cap);
+  if (P->shard) return shard_commit(P, ptrs, lens, outs, statuses, cap);
   return key_commit(P->key, *P->ws, ptrs, lens, outs, statuses, P->stream, cap);
 }
 
@@ -962,13 +962,17 @@ int plk_prover_msm_stats(plk_prover* p, int reset, double* accumulate_ms, uint64
 int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int rank, int world,
                      plk_allgather_fn allgather, void* user) {
   if (!p || world < 1 || rank < 0 || rank >= world) return PLK_E_ARG;
-  if (world > 1 && (!slice || !allgather || slice->ctx->device != p->key->ctx->device))
+  // world 1 with a slice and an all-gather still takes the exchange path (one slice covering
+  // the SRS, one rank's partials exchanged): the whole sharded code path on one GPU. World 1
+  // without them is the unsharded prover.
+  const bool sharded = world > 1 || (slice && allgather);
+  if (sharded && (!slice || !allgather || slice->ctx->device != p->key->ctx->device))
     return PLK_E_ARG;
-  p->shard = world > 1 ? slice : nullptr;
-  p->shard_lo = world > 1 ? slice_start : 0;
+  p->shard = sharded ? slice : nullptr;
+  p->shard_lo = sharded ? slice_start : 0;
   p->rank = rank;
   p->world = world;
-  p->allgather = world > 1 ? allgather : nullptr;
+  p->allgather = sharded ? allgather : nullptr;
   p->allgather_user = user;
   return PLK_OK;
 }

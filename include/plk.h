@@ -292,7 +292,9 @@ int plk_prover_msm_stats(plk_prover* p, int reset, double* accumulate_ms, uint64
  * dusk-plonk_amd/parallel.py): `allgather(user, send, bytes, recv)` must place every rank's
  * `bytes` of `send` at recv + rank * bytes and return 0 (non-zero: PLK_E_DEVICE). Slices
  * must tile [0, N) in rank order with N >= the key's trimmed SRS; every rank calls
- * plk_prover_prove for every proof, in the same order (the exchange is a collective). */
+ * plk_prover_prove for every proof, in the same order (the exchange is a collective).
+ * world = 1 with a slice and an all-gather runs the same exchange path with one rank (the
+ * sharded code path on one GPU); world = 1 with slice = allgather = NULL is unsharded. */
 typedef int (*plk_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
 int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int rank, int world,
                      plk_allgather_fn allgather, void* user);

@@ -506,10 +506,11 @@ def _rccl_world1_worker(rank, world, port, q, logn, lanes):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    checks = {}
     try:
-        ok = dist.get_backend() == "nccl"
+        checks["backend"] = dist.get_backend() == "nccl"
         ag = torch_allgather(None, dev)  # the byte all-gather's device path
-        ok &= ag(b"\x01\x02\x03") == b"\x01\x02\x03"
+        checks["allgather"] = ag(b"\x01\x02\x03") == b"\x01\x02\x03"
         tau = random_fr(1, seed=71)[0]
         ctx = plk.Context.default(0)
         n = 1 << logn
@@ -520,7 +521,7 @@ def _rccl_world1_worker(rank, world, port, q, logn, lanes):
         s = torch.cuda.current_stream().cuda_stream
         got = spp.commit_dev(coef.data_ptr(), n, s, dev)
         want = pp.commit_dev(coef.data_ptr(), n, s)
-        ok &= np.array_equal(got.words, want.words)
+        checks["sharded_commit"] = np.array_equal(got.words, want.words)
 
         def circ(seed):
             cs = Plonk()
@@ -549,11 +550,15 @@ def _rccl_world1_worker(rank, world, port, q, logn, lanes):
         for t in ts:
             t.join(300)
         svc.close()
-        ok &= not errors and all(results.get(s_) == want[s_] for s_ in seeds)
-        ok &= svc.requests == 4 * len(seeds)  # 4 commit groups per proof
+        checks["errors"] = errors
+        checks["proofs"] = [results.get(s_) == want[s_] for s_ in seeds]
+        checks["requests"] = (svc.requests, svc.exchanges)  # 4 commit groups per proof
         for ln in lns:
             ln.close()
-        q.put((rank, bool(ok)))
+        q.put((rank, checks))
+    except Exception as e:  # noqa: BLE001
+        checks["exception"] = repr(e)
+        q.put((rank, checks))
     finally:
         dist.destroy_process_group()
 
@@ -561,5 +566,9 @@ def _rccl_world1_worker(rank, world, port, q, logn, lanes):
 @pytest.mark.gpu
 def test_sharded_prover_rccl_world1(plk, gpu_ctx):
     """3 lanes sharded over an RCCL world of one (the device-tensor exchange runs for real)."""
-    out = _spawn(_rccl_world1_worker, 1, 14, 3)
-    assert out == {0: True}
+    c = _spawn(_rccl_world1_worker, 1, 14, 3)[0]
+    print(c)
+    assert "exception" not in c, c
+    assert c["backend"] and c["allgather"] and c["sharded_commit"], c
+    assert not c["errors"] and all(c["proofs"]) and len(c["proofs"]) == 6, c
+    assert c["requests"][0] == 4 * 6 and 1 <= c["requests"][1] <= 4 * 6, c
