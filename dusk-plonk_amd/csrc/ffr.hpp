@@ -172,14 +172,16 @@ struct RxMultipleK {
 #ifndef PLK_RX_PIN
 #define PLK_RX_PIN 0
 #endif
-// acc += x * y as ONE v_mad_u64_u32 on the running column accumulator. With PLK_RX_PIN the
-// accumulator passes an empty asm after each step, so LLVM cannot reassociate a column's
-// additions (it otherwise sums a column's products into a fresh accumulator and adds the
-// carried one with a 64-bit v_lshl_add_u64 per column).
+// acc += x * y as ONE v_mad_u64_u32 on the running column accumulator. With PLK_RX_PIN
+// (experiment, off) each step is followed by a use-only empty asm, so LLVM's reassociation
+// cannot split a column (it otherwise sums a column's products into a fresh accumulator and
+// adds the carried one with a 64-bit v_lshl_add_u64 per column): 4 401 instead of 4 579
+// instructions per mixed addition, but one dependent chain per product measured 3-4 %
+// SLOWER (6.02-6.14e9 against 6.28-6.35e9 additions/s, profiles/r04_ubench_acc_pins.txt).
 PLK_RX void rx_madd(uint64_t& acc, uint32_t x, uint32_t y) {
   acc += (uint64_t)x * y;
 #if PLK_RX_PIN
-  __asm__("" : "+v"(acc));
+  __asm__ volatile("" ::"v"(acc));
 #endif
 }
 
@@ -397,6 +399,12 @@ PLK_RX Rx<C> rx_sqr(const Rx<C>& a) {
 // bounds). Same results as rx_mul / rx_sqr / rx_mul_add, bit for bit.
 enum : int { kRxMul = 0, kRxSqr = 1, kRxMulAdd = 2 };
 
+// "+v": the accumulator is redefined by the (empty) asm, so the next step of the chain
+// depends on it and the volatile asms keep the interleaved order. The hazard recognizer then
+// pads a chain's next mad with one s_nop when fewer than three instructions separate it
+// from the asm (two-product groups): one wait cycle, against the 64-bit merge add per column
+// it replaces. A use-only pin ("v" input) leaves the order to the scheduler, which
+// regroups the chains: measured no faster than the plain code (profiles/r04_ubench_acc_pins.txt).
 PLK_RX void rx_pin(uint64_t& v) { __asm__ volatile("" : "+v"(v)); }
 
 template <class C, int NP>
