@@ -430,6 +430,7 @@ constexpr RxColOrder<sizeof...(KINDS)> rx_col_order() {
   constexpr int kind[NP] = {KINDS...};
   constexpr RxPlan<C, 1> P1{};
   constexpr RxPlan<C, 2> P2{};
+  constexpr bool SPLIT_ON = RxSplitOn<C>::value;
   const int i0 = K < L ? 0 : K - L + 1, i1 = K < L ? K : L - 1;
   const int n1 = i1 - i0 + 1;
   const int ncross = (K + 1) / 2 - i0 > 0 ? (K + 1) / 2 - i0 : 0;
@@ -438,7 +439,7 @@ constexpr RxColOrder<sizeof...(KINDS)> rx_col_order() {
     if (i < K || K >= L) ++nred;
   int left[3 * NP] = {};
   for (int p = 0; p < NP; ++p) {
-    const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+    const bool split = SPLIT_ON && (kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K]);
     const int prod = kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? ncross + ((K & 1) == 0 ? 1 : 0) : 2 * n1;
     if (!split) {
       left[3 * p] = prod + nred;
@@ -478,6 +479,7 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
   constexpr RxConst<C> KC = RxK<C>::k;
   constexpr RxPlan<C, 1> P1 = RxPlanK<C, 1>::k;
   constexpr RxPlan<C, 2> P2 = RxPlanK<C, 2>::k;
+  constexpr bool SPLIT_ON = RxSplitOn<C>::value;  // Fr (9 x 29): one accumulator per column
   constexpr int i0 = K < L ? 0 : K - L + 1, i1 = K < L ? K : L - 1;
   constexpr int n1 = i1 - i0 + 1;                                      // terms of one a*b column
   constexpr int ncross = (K + 1) / 2 - i0 > 0 ? (K + 1) / 2 - i0 : 0;  // a^2: i0 <= i, 2i < K
@@ -495,7 +497,7 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
 #pragma unroll
   for (int e = 0; e < ord.n; ++e) {
     const int q = ord.acc[e], p = q / 3, which = q % 3;
-    const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+    const bool split = SPLIT_ON && (kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K]);
     const int t = pos[q]++;
     uint64_t& dst = which == 0 ? g.acc[p] : which == 1 ? s2[p] : s3[p];
     // the accumulator's t-th term
@@ -519,7 +521,7 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
   (void)rlast;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+    const bool split = SPLIT_ON && (kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K]);
     rx_column_close<C>(split, K, g.acc[p], s2[p], s3[p], g.m[p], *out[p]);
   }
 }

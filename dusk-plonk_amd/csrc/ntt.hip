@@ -80,6 +80,14 @@ constexpr bool kR2First = PLK_NTT_R2FIRST != 0;
 #define PLK_NTT_R4FIRST 0
 #endif
 constexpr bool kR4First = PLK_NTT_R4FIRST != 0;
+// The radix-4 step's four products as interleaved chains (ffr.hpp rx_prod_group, round 4):
+// 2 = two pairs (default), 1 = a triple (y2, y3, o1) then o3 alone, 0 = one by one (round 3).
+// Loop VALU cycles 4 137 (0) -> 3 914 (1) / 3 865 (2); measured dft + idft per step, 2^20:
+// 0.299-0.301 / 0.292-0.297 / 0.291-0.299 ms, 2^23: 2.036-2.045 / 2.007-2.015 / 1.987-1.996 ms
+// (profiles/r04_ntt_grouped_ab.jsonl; proofs within noise)
+#ifndef PLK_NTT_GROUPED
+#define PLK_NTT_GROUPED 2
+#endif
 // k_ntt_pass minimum waves per SIMD (-DPLK_NTT_MINW=4 caps it at 128 VGPRs)
 #ifndef PLK_NTT_MINW
 #define PLK_NTT_MINW 1
@@ -239,6 +247,25 @@ __device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uin
     // interleave. Stage of half h: twiddle w^(r s2) for both pairs; outputs normalised
     const RFr w1 = lds_ld(twl, TS, r << sh1), w2 = lds_ld(twl, TS, (r + h) << sh1);
     const RFr w = lds_ld(twl, TS, r << sh2);
+#if PLK_NTT_GROUPED
+    // the step's two pairs of independent products as interleaved chains (ffr.hpp
+    // rx_prod_group): no 64-bit merge add per column
+    RFr y2, y3, o1;
+#if PLK_NTT_GROUPED == 2
+    rx_mul2(rx_sub_u<FrCfg, 6>(x0, x2), w1, rx_sub_u<FrCfg, 6>(x1, x3), w2, y2, y3);  // < 2r
+    RFr o3;
+    rx_mul2(sub_u2<11>(y0, y1), w, rx_sub_u<FrCfg, 5>(y2, y3), w, o1, o3);
+#else
+    // (y0 - y1 + 11r) w needs no product of this step: three independent chains
+    rx_mul3(rx_sub_u<FrCfg, 6>(x0, x2), w1, rx_sub_u<FrCfg, 6>(x1, x3), w2, sub_u2<11>(y0, y1), w,
+            y2, y3, o1);  // < 2r
+    const RFr o3 = rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w);
+#endif
+    lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
+    lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 4r
+    lds_std<DS>(data, i1, o1);
+    lds_std<DS>(data, i3, o3);
+#else
     const RFr y2 = rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), w1);  // < 2r
     const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), w2);
     const RFr o1 = rx_mul(sub_u2<11>(y0, y1), w);          // (y0 - y1 + 11r) w
@@ -246,6 +273,7 @@ __device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uin
     lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 4r
     lds_std<DS>(data, i1, o1);
     lds_std<DS>(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 2r
+#endif
   }
 }
 

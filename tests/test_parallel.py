@@ -572,3 +572,44 @@ def test_sharded_prover_rccl_world1(plk, gpu_ctx):
     assert c["backend"] and c["allgather"] and c["sharded_commit"], c
     assert not c["errors"] and all(c["proofs"]) and len(c["proofs"]) == 6, c
     assert c["requests"][0] == 4 * 6 and 1 <= c["requests"][1] <= 4 * 6, c
+
+
+@pytest.mark.gpu
+def test_rccl_in_process_device_exchange(plk, gpu_ctx):
+    """RCCL (torch.distributed `nccl`) in the test process itself at world size 1: the
+    device-tensor paths of the exchange (torch_allgather, gather_fold, ExchangeService with a
+    device) run over librccl here, then the group is torn down."""
+    import threading
+    import torch
+    import torch.distributed as dist
+    from dusk_plonk_amd.parallel import ExchangeService, gather_fold, torch_allgather
+    if dist.is_initialized():
+        pytest.skip("a process group already exists in this process")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        assert torch_allgather(None, dev)(b"rccl") == b"rccl"
+        g = dict(np.load(ROOT / "tests" / "golden" / "msm_golden.npz", allow_pickle=False))
+        part = np.stack([g["random_result"], g["sparse_result"]])
+        res = gather_fold(part, [plk.PLK_OK, plk.PLK_OK], None, dev)
+        assert np.array_equal(res[0].words, g["random_result"])
+        assert np.array_equal(res[1].words, g["sparse_result"])
+        svc = ExchangeService(None, dev)
+        out = {}
+
+        def lane(i):
+            ag = svc.allgather_for(i)
+            out[i] = [ag(bytes([i, j]) * (j + 1)) for j in range(5)]
+        ts = [threading.Thread(target=lane, args=(i,)) for i in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        svc.close()
+        assert all(out[i] == [bytes([i, j]) * (j + 1) for j in range(5)] for i in range(3))
+        assert svc.requests == 15
+    finally:
+        dist.destroy_process_group()
