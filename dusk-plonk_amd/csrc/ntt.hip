@@ -80,6 +80,19 @@ constexpr bool kR2First = PLK_NTT_R2FIRST != 0;
 #define PLK_NTT_R4FIRST 0
 #endif
 constexpr bool kR4First = PLK_NTT_R4FIRST != 0;
+// The last two radix-4 steps of a pass (halves 8, 4 then 2, 1) exchange data only inside
+// 16-row blocks of one column, between the 4 groups (t, 16B + r), r < 4. PLK_NTT_QUADX puts
+// those 4 groups on the 4 lanes of a quad (group index r lowest) and: 1 = exchanges through
+// LDS without the workgroup barrier (the producer and consumer lanes are in one wave);
+// 2 = exchanges in registers (DPP quad transpose, quad_transpose) with no LDS round trip;
+// 0 = off (one barrier and LDS round trip per step). Measured (profiles/r04_ntt_quadx_ab.jsonl,
+// one box, interleaved, dft + idft per step): 2^20 0.3078-0.3079 / 0.3028-0.3033 / 0.2981-0.3058
+// ms, 2^23 2.095-2.099 / 2.083-2.086 / 2.045-2.048 ms, 2^17 within noise, 2^20 proofs
+// 31.6-32.0 / 32.5-32.7 / 32.3-32.9 M constraints/s: the DPP exchange (+13 % VALU cycles in
+// the loop body) still beats the LDS round trip and barrier it removes. Default 2.
+#ifndef PLK_NTT_QUADX
+#define PLK_NTT_QUADX 2
+#endif
 // The radix-4 step's four products as interleaved chains (ffr.hpp rx_prod_group, round 4):
 // 2 = two pairs (default), 1 = a triple (y2, y3, o1) then o3 alone, 0 = one by one (round 3).
 // Loop VALU cycles 4 137 (0) -> 3 914 (1) / 3 865 (2); measured dft + idft per step, 2^20:
@@ -223,23 +236,22 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
 }
 
 // Two radix-2 DIF stages (halves 2h and h) on rows x0..x3 = j, j+h, j+2h, j+3h of one
-// column (r = j mod h), stored back to LDS at i0..i3. Inputs normalised, < 5r.
-template <uint32_t DS>
-__device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uint32_t TS,
-                                        const uint32_t* ztab, uint32_t r, uint32_t h,
-                                        uint32_t sh1, uint32_t sh2, uint32_t i0, uint32_t i1,
-                                        uint32_t i2, uint32_t i3, const RFr& x0, const RFr& x1,
-                                        const RFr& x2, const RFr& x3) {
+// column (r = j mod h); outputs o0..o3 belong at rows j, j+h, j+2h, j+3h. Inputs normalised,
+// < 5r; outputs normalised, < 4r.
+__device__ __forceinline__ void r4_math(const uint32_t* twl, uint32_t TS, const uint32_t* ztab,
+                                        uint32_t r, uint32_t h, uint32_t sh1, uint32_t sh2,
+                                        const RFr& x0, const RFr& x1, const RFr& x2,
+                                        const RFr& x3, RFr& o0, RFr& o1, RFr& o2, RFr& o3) {
   // inputs: normalised, < 5r. Stage of half 2h: twiddle w^(r s1) for x0/x2 (identity
   // when r = 0), w^((r+h) s1) for x1/x3; sums y0, y1 unnormalised (limbs < 2^30, < 10r)
   const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
   if (h == 1) {  // r = 0 in every group: no twiddle on x0 / x2 nor in the second stage
     const RFr y2 = reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 4r
     const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, 1u << sh1));
-    lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));            // < 20r -> < 4r
-    lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));            // < 6r -> < 4r
-    lds_std<DS>(data, i1, reduce_q(sub_u2<11>(y0, y1), ztab));       // < 21r -> < 4r
-    lds_std<DS>(data, i3, reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab));
+    o0 = reduce_q(add_u(y0, y1), ztab);             // < 20r -> < 4r
+    o2 = reduce_q(add_u(y2, y3), ztab);             // < 6r -> < 4r
+    o1 = reduce_q(sub_u2<11>(y0, y1), ztab);        // < 21r -> < 4r
+    o3 = reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab);
   } else {
     // r = 0 groups multiply by w^0 = 1 (twl[0]) under the same bounds as r != 0: the
     // lanes of a wave mix both (columns T < 64), so a branch ran both paths, and
@@ -248,32 +260,59 @@ __device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uin
     const RFr w1 = lds_ld(twl, TS, r << sh1), w2 = lds_ld(twl, TS, (r + h) << sh1);
     const RFr w = lds_ld(twl, TS, r << sh2);
 #if PLK_NTT_GROUPED
-    // the step's two pairs of independent products as interleaved chains (ffr.hpp
-    // rx_prod_group): no 64-bit merge add per column
-    RFr y2, y3, o1;
+    // the step's independent products as interleaved chains (ffr.hpp rx_prod_group): no
+    // 64-bit merge add per column
+    RFr y2, y3;
 #if PLK_NTT_GROUPED == 2
     rx_mul2(rx_sub_u<FrCfg, 6>(x0, x2), w1, rx_sub_u<FrCfg, 6>(x1, x3), w2, y2, y3);  // < 2r
-    RFr o3;
     rx_mul2(sub_u2<11>(y0, y1), w, rx_sub_u<FrCfg, 5>(y2, y3), w, o1, o3);
 #else
     // (y0 - y1 + 11r) w needs no product of this step: three independent chains
     rx_mul3(rx_sub_u<FrCfg, 6>(x0, x2), w1, rx_sub_u<FrCfg, 6>(x1, x3), w2, sub_u2<11>(y0, y1), w,
             y2, y3, o1);  // < 2r
-    const RFr o3 = rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w);
+    o3 = rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w);
 #endif
-    lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
-    lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 4r
-    lds_std<DS>(data, i1, o1);
-    lds_std<DS>(data, i3, o3);
 #else
     const RFr y2 = rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), w1);  // < 2r
     const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), w2);
-    const RFr o1 = rx_mul(sub_u2<11>(y0, y1), w);          // (y0 - y1 + 11r) w
-    lds_std<DS>(data, i0, reduce_q(add_u(y0, y1), ztab));  // < 20r -> < 4r
-    lds_std<DS>(data, i2, reduce_q(add_u(y2, y3), ztab));  // < 4r
-    lds_std<DS>(data, i1, o1);
-    lds_std<DS>(data, i3, rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w));  // y3 < 2r
+    o1 = rx_mul(sub_u2<11>(y0, y1), w);                    // (y0 - y1 + 11r) w
+    o3 = rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w);            // y3 < 2r
 #endif
+    o0 = reduce_q(add_u(y0, y1), ztab);  // < 20r -> < 4r
+    o2 = reduce_q(add_u(y2, y3), ztab);  // < 4r
+  }
+}
+
+// r4_math, outputs stored back to LDS at i0..i3
+template <uint32_t DS>
+__device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uint32_t TS,
+                                        const uint32_t* ztab, uint32_t r, uint32_t h,
+                                        uint32_t sh1, uint32_t sh2, uint32_t i0, uint32_t i1,
+                                        uint32_t i2, uint32_t i3, const RFr& x0, const RFr& x1,
+                                        const RFr& x2, const RFr& x3) {
+  RFr o0, o1, o2, o3;
+  r4_math(twl, TS, ztab, r, h, sh1, sh2, x0, x1, x2, x3, o0, o1, o2, o3);
+  lds_std<DS>(data, i0, o0);
+  lds_std<DS>(data, i2, o2);
+  lds_std<DS>(data, i1, o1);
+  lds_std<DS>(data, i3, o3);
+}
+
+// 4 x 4 transpose of (a0..a3) over the lanes of a quad: lane q ends with element q of lanes
+// 0..3 (DPP quad_perm xor 1, then xor 2; lane-dependent selects around each move)
+__device__ __forceinline__ void quad_transpose(RFr& a0, RFr& a1, RFr& a2, RFr& a3) {
+  const uint32_t lane = __lane_id();
+  const bool b0 = lane & 1u, b1 = lane & 2u;
+#pragma unroll
+  for (int l = 0; l < kL; ++l) {
+    const uint32_t s01 = b0 ? a0.v[l] : a1.v[l], s23 = b0 ? a2.v[l] : a3.v[l];
+    const uint32_t r01 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s01, 0xB1, 0xF, 0xF, false);
+    const uint32_t r23 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s23, 0xB1, 0xF, 0xF, false);
+    if (b0) { a0.v[l] = r01; a2.v[l] = r23; } else { a1.v[l] = r01; a3.v[l] = r23; }
+    const uint32_t s02 = b1 ? a0.v[l] : a2.v[l], s13 = b1 ? a1.v[l] : a3.v[l];
+    const uint32_t r02 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s02, 0x4E, 0xF, 0xF, false);
+    const uint32_t r13 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s13, 0x4E, 0xF, 0xF, false);
+    if (b1) { a0.v[l] = r02; a1.v[l] = r13; } else { a2.v[l] = r02; a3.v[l] = r13; }
   }
 }
 
@@ -474,8 +513,37 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   for (; lh >= 1; lh -= 2) {
     const uint32_t h = 1u << (lh - 1);
     const uint32_t sh1 = lr - 1 - lh, sh2 = lr - lh;  // twiddle index shifts of both stages
+    // the last two steps with their groups of a 16-row block on one quad (PLK_NTT_QUADX)
+    const bool quad = PLK_NTT_QUADX != 0 && (lh == 3 || lh == 1) && lr >= 5 &&
+                      (E >> 2) % bd == 0;
+    if (PLK_NTT_QUADX == 2 && quad && lh == 3) {
+      // halves 8 and 4, quad transpose in registers, halves 2 and 1: one LDS round trip
+      for (uint32_t g = tid; g < (E >> 2); g += bd) {
+        const uint32_t r = g & 3u, t = (g >> 2) & (T - 1), B = g >> (2 + lt);
+        const uint32_t j = (B << 4) + r;  // rows j + 4m of the 16-row block B
+        RFr x0 = lds_ldd<DS>(data, (j << lt) + t), x1 = lds_ldd<DS>(data, ((j + 4) << lt) + t);
+        RFr x2 = lds_ldd<DS>(data, ((j + 8) << lt) + t), x3 = lds_ldd<DS>(data, ((j + 12) << lt) + t);
+        RFr o0, o1, o2, o3;
+        r4_math(twl, TS, ztab, r, 4, lr - 4, lr - 3, x0, x1, x2, x3, o0, o1, o2, o3);
+        quad_transpose(o0, o1, o2, o3);  // lane r now holds rows 16B + 4r + (0, 1, 2, 3)
+        const uint32_t jq = (B << 4) + (r << 2);
+        r4_step<DS>(data, twl, TS, ztab, 0, 1, lr - 2, lr - 1, (jq << lt) + t,
+                    ((jq + 1) << lt) + t, ((jq + 2) << lt) + t, ((jq + 3) << lt) + t, o0, o1, o2,
+                    o3);
+      }
+      lh -= 2;  // both steps done
+      __syncthreads();
+      continue;
+    }
     for (uint32_t g = tid; g < (E >> 2); g += bd) {
-      const uint32_t t = g & (T - 1), jg = g >> lt;
+      uint32_t t, jg;
+      if (quad) {  // r lowest: the 4 groups of a (column, 16-row block) on one quad
+        t = (g >> 2) & (T - 1);
+        jg = ((g >> (2 + lt)) << 2) + (g & 3u);
+      } else {
+        t = g & (T - 1);
+        jg = g >> lt;
+      }
       const uint32_t r = jg & (h - 1);
       const uint32_t j = ((jg >> (lh - 1)) << (lh + 1)) + r;
       const uint32_t i0 = (j << lt) + t, i1 = ((j + h) << lt) + t;
@@ -484,7 +552,14 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
       const RFr x2 = lds_ldd<DS>(data, i2), x3 = lds_ldd<DS>(data, i3);
       r4_step<DS>(data, twl, TS, ztab, r, h, sh1, sh2, i0, i1, i2, i3, x0, x1, x2, x3);
     }
-    __syncthreads();
+    if (PLK_NTT_QUADX == 1 && quad && lh == 3) {
+      // the next step reads only what this wave's own quads wrote: LDS writes of a wave are
+      // visible to its lanes once they complete — no workgroup barrier
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      __syncthreads();
+    }
   }
   if (lh == 0) {  // odd radix: last stage of half 1 (twiddle-free)
     for (uint32_t b = tid; b < (E >> 1); b += bd) {
