@@ -835,6 +835,82 @@ PLK_HD Fe<C> fe_to_rx_domain(Fe<C> x) {
   return x;
 }
 
+// ---- constant-operand (Shoup) product in Fr, for the NTT twiddles ----------------------
+// x * w mod r for a constant w (canonical, plain — not Montgomery) with the precomputed
+// w' = floor(w 2^261 / r): q = floor(x w' / 2^261) from the high columns only (7 .. 16 of
+// the 18: the dropped ones are worth < 2^-23 of q, so q is exact or one low), then
+// z = x w - q r computed mod 2^261 as x w + q (2^261 - r) in the low 9 columns. 53 + 45 + 45
+// mads against Montgomery's 81 + 81, and no per-column digit multiply. x: limbs below 2^31,
+// value below 2^261 (every NTT multiplicand); w, w' normalised. Output normalised, [0, 3r)
+// (Shoup's [0, 2r) plus one r for the approximate q). Columns stay below 2^64: 9 products
+// below 2^60 plus 9 below 2^58.
+struct FrShoupK {
+  uint32_t rbar[9];  // 2^261 - r
+  uint32_t rinv[9];  // r^-1 mod 2^261
+};
+constexpr FrShoupK kFrShoup = {
+    {0x1fffffffu, 0x7u, 0x690040u, 0x4b7fa00u, 0x27faac4u, 0x13fbfb2fu, 0xadf3318u, 0x159acc50u,
+     0x1f8c1258u},
+    {0x1u, 0x8u, 0x690080u, 0xb480000u, 0x113f9ac4u, 0x9f47ffdu, 0x1f1b9f93u, 0x9e5081au,
+     0x1fc2bbc5u}};
+
+PLK_RX Rx<FrCfg> fr_shoup(const Rx<FrCfg>& x, const Rx<FrCfg>& w, const Rx<FrCfg>& wp) {
+  constexpr int L = 9, B = 29;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t q[L];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 7; k < 2 * L - 1; ++k) {  // high columns of x w'
+#pragma unroll
+    for (int i = 0; i < L; ++i)
+      if (k - i >= 0 && k - i < L) acc += (uint64_t)x.v[i] * wp.v[k - i];
+    if (k >= L) q[k - L] = (uint32_t)acc & MASK;
+    acc >>= B;
+  }
+  q[L - 1] = (uint32_t)acc;
+  Rx<FrCfg> z;
+  acc = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {  // low columns of x w + q (2^261 - r)
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc += (uint64_t)x.v[i] * w.v[k - i];
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc += (uint64_t)q[i] * kFrShoup.rbar[k - i];
+    z.v[k] = (uint32_t)acc & MASK;
+    acc >>= B;
+  }
+  return z;
+}
+
+// (w, w') from rho = w R' mod r (canonical, an R'-domain twiddle table entry): w = rho / R',
+// brought to [0, r); w' = floor(w 2^261 / r) = (2^261 - rho) r^-1 mod 2^261, since
+// w 2^261 = w' r + rho exactly.
+PLK_RX void fr_shoup_prep(const Rx<FrCfg>& rho, Rx<FrCfg>& w, Rx<FrCfg>& wp) {
+  constexpr int L = 9, B = 29;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  Rx<FrCfg> one = rx_zero<FrCfg>();
+  one.v[0] = 1;
+  w = rx_unpack(rx_pack_canonical(rx_mul(rho, one)));
+  // 2^261 - rho, normalised (rho < r < 2^261)
+  Rx<FrCfg> n;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int32_t t = br - (int32_t)rho.v[i];
+    n.v[i] = (uint32_t)t & MASK;
+    br = t >> B;  // 0 or -1
+  }
+  // low 261 bits of n * rinv
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc += (uint64_t)n.v[i] * kFrShoup.rinv[k - i];
+    wp.v[k] = (uint32_t)acc & MASK;
+    acc >>= B;
+  }
+}
+
 #undef PLK_RX
 
 }  // namespace plk

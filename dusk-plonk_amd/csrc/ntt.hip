@@ -94,8 +94,9 @@ constexpr bool kR4First = PLK_NTT_R4FIRST != 0;
 #define PLK_NTT_QUADX 2
 #endif
 // The radix-4 step's four products as interleaved chains (ffr.hpp rx_prod_group, round 4):
-// 2 = two pairs (default), 1 = a triple (y2, y3, o1) then o3 alone, 0 = one by one (round 3).
-// Loop VALU cycles 4 137 (0) -> 3 914 (1) / 3 865 (2); measured dft + idft per step, 2^20:
+// nonzero = two pairs (default; round 4 also measured a triple (y2, y3, o1) then o3 alone),
+// 0 = one by one (round 3). Loop VALU cycles 4 137 (one by one) -> 3 914 (triple) / 3 865
+// (pairs); measured dft + idft per step, 2^20:
 // 0.299-0.301 / 0.292-0.297 / 0.291-0.299 ms, 2^23: 2.036-2.045 / 2.007-2.015 / 1.987-1.996 ms
 // (profiles/r04_ntt_grouped_ab.jsonl; proofs within noise)
 #ifndef PLK_NTT_GROUPED
@@ -235,6 +236,33 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
   return r;
 }
 
+// Products by the inner (stage) twiddles staged in LDS. PLK_NTT_SHOUP: the table holds
+// (w, w' = floor(w 2^261 / r)) planes and the product is the constant-operand Shoup form
+// (ffr.hpp fr_shoup, 143 mads, output < 3r); otherwise Montgomery by w R' (rx_mul, < 2r).
+#ifndef PLK_NTT_SHOUP
+#define PLK_NTT_SHOUP 0
+#endif
+constexpr uint32_t kTwPlanes = PLK_NTT_SHOUP ? 2 : 1;  // twiddle plane sets in LDS
+__device__ __forceinline__ RFr twmul(const RFr& a, const uint32_t* twl, uint32_t TS, uint32_t idx) {
+#if PLK_NTT_SHOUP
+  return fr_shoup(a, lds_ld(twl, TS, idx), lds_ld(twl + kL * TS, TS, idx));
+#else
+  return rx_mul(a, lds_ld(twl, TS, idx));
+#endif
+}
+__device__ __forceinline__ void twmul2(const RFr& a0, uint32_t i0, const RFr& a1, uint32_t i1,
+                                       const uint32_t* twl, uint32_t TS, RFr& o0, RFr& o1) {
+#if PLK_NTT_SHOUP
+  o0 = fr_shoup(a0, lds_ld(twl, TS, i0), lds_ld(twl + kL * TS, TS, i0));
+  o1 = fr_shoup(a1, lds_ld(twl, TS, i1), lds_ld(twl + kL * TS, TS, i1));
+#elif PLK_NTT_GROUPED
+  rx_mul2(a0, lds_ld(twl, TS, i0), a1, lds_ld(twl, TS, i1), o0, o1);
+#else
+  o0 = rx_mul(a0, lds_ld(twl, TS, i0));
+  o1 = rx_mul(a1, lds_ld(twl, TS, i1));
+#endif
+}
+
 // Two radix-2 DIF stages (halves 2h and h) on rows x0..x3 = j, j+h, j+2h, j+3h of one
 // column (r = j mod h); outputs o0..o3 belong at rows j, j+h, j+2h, j+3h. Inputs normalised,
 // < 5r; outputs normalised, < 4r.
@@ -247,39 +275,25 @@ __device__ __forceinline__ void r4_math(const uint32_t* twl, uint32_t TS, const 
   const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
   if (h == 1) {  // r = 0 in every group: no twiddle on x0 / x2 nor in the second stage
     const RFr y2 = reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 4r
-    const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), lds_ld(twl, TS, 1u << sh1));
+    const RFr y3 = twmul(rx_sub_u<FrCfg, 6>(x1, x3), twl, TS, 1u << sh1);  // < 3r
     o0 = reduce_q(add_u(y0, y1), ztab);             // < 20r -> < 4r
-    o2 = reduce_q(add_u(y2, y3), ztab);             // < 6r -> < 4r
+    o2 = reduce_q(add_u(y2, y3), ztab);             // < 7r -> < 4r
     o1 = reduce_q(sub_u2<11>(y0, y1), ztab);        // < 21r -> < 4r
     o3 = reduce_q(rx_sub_u<FrCfg, 5>(y2, y3), ztab);
   } else {
     // r = 0 groups multiply by w^0 = 1 (twl[0]) under the same bounds as r != 0: the
     // lanes of a wave mix both (columns T < 64), so a branch ran both paths, and
     // straight-line code leaves three independent products (y2, y3, output 1) to
-    // interleave. Stage of half h: twiddle w^(r s2) for both pairs; outputs normalised
-    const RFr w1 = lds_ld(twl, TS, r << sh1), w2 = lds_ld(twl, TS, (r + h) << sh1);
-    const RFr w = lds_ld(twl, TS, r << sh2);
-#if PLK_NTT_GROUPED
-    // the step's independent products as interleaved chains (ffr.hpp rx_prod_group): no
-    // 64-bit merge add per column
+    // interleave. Stage of half h: twiddle w^(r s2) for both pairs; outputs normalised.
+    // The step's products go as interleaved pairs (twmul2: ffr.hpp rx_prod_group, no 64-bit
+    // merge add per column) unless PLK_NTT_GROUPED = 0. Products < 2r (< 3r with Shoup).
     RFr y2, y3;
-#if PLK_NTT_GROUPED == 2
-    rx_mul2(rx_sub_u<FrCfg, 6>(x0, x2), w1, rx_sub_u<FrCfg, 6>(x1, x3), w2, y2, y3);  // < 2r
-    rx_mul2(sub_u2<11>(y0, y1), w, rx_sub_u<FrCfg, 5>(y2, y3), w, o1, o3);
-#else
-    // (y0 - y1 + 11r) w needs no product of this step: three independent chains
-    rx_mul3(rx_sub_u<FrCfg, 6>(x0, x2), w1, rx_sub_u<FrCfg, 6>(x1, x3), w2, sub_u2<11>(y0, y1), w,
-            y2, y3, o1);  // < 2r
-    o3 = rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w);
-#endif
-#else
-    const RFr y2 = rx_mul(rx_sub_u<FrCfg, 6>(x0, x2), w1);  // < 2r
-    const RFr y3 = rx_mul(rx_sub_u<FrCfg, 6>(x1, x3), w2);
-    o1 = rx_mul(sub_u2<11>(y0, y1), w);                    // (y0 - y1 + 11r) w
-    o3 = rx_mul(rx_sub_u<FrCfg, 5>(y2, y3), w);            // y3 < 2r
-#endif
+    twmul2(rx_sub_u<FrCfg, 6>(x0, x2), r << sh1, rx_sub_u<FrCfg, 6>(x1, x3), (r + h) << sh1, twl, TS,
+           y2, y3);
+    // (y0 - y1 + 11r) w and (y2 - y3 + 5r) w
+    twmul2(sub_u2<11>(y0, y1), r << sh2, rx_sub_u<FrCfg, 5>(y2, y3), r << sh2, twl, TS, o1, o3);
     o0 = reduce_q(add_u(y0, y1), ztab);  // < 20r -> < 4r
-    o2 = reduce_q(add_u(y2, y3), ztab);  // < 4r
+    o2 = reduce_q(add_u(y2, y3), ztab);  // < 6r -> < 4r
   }
 }
 
@@ -342,7 +356,7 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   const uint32_t TS = PRUNE ? R : H;
   uint32_t* data = smem32;          // kL planes of E (stride DS >= E)
   uint32_t* twl = smem32 + kL * DS;
-  uint32_t* ztab = twl + kL * TS;   // kZTab (reduce_q)
+  uint32_t* ztab = twl + kTwPlanes * kL * TS;  // kZTab (reduce_q)
 
   // vector blockIdx.y of a batch: its input, output and scale-table rows (NttBatch::group)
   {
@@ -357,7 +371,16 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   const uint32_t nr_log = log_n - lr;  // log2(N/R)
 
-  for (uint32_t x = tid; x < TS; x += bd) lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
+  for (uint32_t x = tid; x < TS; x += bd) {
+#if PLK_NTT_SHOUP
+    RFr w, wp;
+    fr_shoup_prep(ld_rfr(&tw[(size_t)x << nr_log]), w, wp);
+    lds_st(twl, TS, x, w);
+    lds_st(twl + kL * TS, TS, x, wp);
+#else
+    lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
+#endif
+  }
   for (uint32_t x = tid; x < kQMax * kL; x += bd) ztab[x] = kZTab.v[x];
 
   // every load of the thread's (at most kLoadIt, E / bd <= 4) elements is issued before the
@@ -439,8 +462,13 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q) {
         const uint32_t blk = 4 * hs + q, b = bitrev(blk, 3);
+#if PLK_NTT_SHOUP  // rx_add wants [0, 2r): the Shoup products (< 3r) go through reduce_q
+        RFr v = (j == 0 || b == 0) ? x : reduce_q(twmul(x, twl, TS, j * b), ztab);
+        if (has8) v = rx_add(v, b == 0 ? x8 : reduce_q(twmul(x8, twl, TS, R8 * b), ztab));
+#else
         RFr v = (j == 0 || b == 0) ? x : rx_mul(x, lds_ld(twl, TS, j * b));
         if (has8) v = rx_add(v, b == 0 ? x8 : rx_mul(x8, lds_ld(twl, TS, R8 * b)));
+#endif
         lds_std<DS>(data, ((blk * R8 + j) << lt) + t, v);
       }
     }
@@ -494,7 +522,7 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
           const uint32_t el = e - (E >> 1);
           const RFr a = lds_ldd<DS>(data, el);
           lds_std<DS>(data, el, reduce_q(add_u(a, v), ztab));                        // < 1.6r
-          lds_std<DS>(data, e, rx_mul(sub_u(a, v), lds_ld(twl, TS, el >> lt)));      // < 2r
+          lds_std<DS>(data, e, twmul(sub_u(a, v), twl, TS, el >> lt));  // < 2r (3r Shoup)
         } else if (e < E) {
           lds_std<DS>(data, e, v);
         }
@@ -819,7 +847,8 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     // (round 3: an LDS floor of 54 / 80 KB per workgroup, i.e. 2 - 3 resident workgroups per
     // CU so that a lone transform's tiles run in staggered generations, measured 3 - 7 %
     // slower at 2^20 and 2^23: the lost occupancy costs more than the overlap gains)
-    const size_t lds = ((size_t)(small ? kDSSmall : kDS) + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
+    const size_t lds = ((size_t)(small ? kDSSmall : kDS) +
+                        kTwPlanes * ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
                        kL * sizeof(uint32_t);
     // persistent software-pipelined passes (k_ntt_pass PF): a lone large transform's grid of
     // pf_grid workgroups, each taking blocks / pf_grid tiles (PLK_NTT_PF = the grid size, 0 off)
