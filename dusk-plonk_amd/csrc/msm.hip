@@ -401,6 +401,115 @@ __global__ void __launch_bounds__(1024) k_sort_small(uint32_t* __restrict__ bloc
   }
 }
 
+// Small batches (B <= kSortSmallMax and at most kSortOneMax scalars per slot: the 2^12-size
+// proofs' commits) sorted by ONE workgroup per slot in ONE dispatch instead of three (k_hist,
+// k_sort_small, k_scatter) or four (with k_any_nonzero): the commit degree check, an LDS
+// histogram over all of the slot's digits, the scans and task records of k_sort_small, then
+// the scatter with LDS cursors. Small proofs are bound by the command processor's dispatch
+// rate, so the dispatches matter more than the single workgroup's latency. The
+// order of the entries inside a bucket differs from the multi-workgroup sort; the bucket's
+// sum (exact XYZZ arithmetic, canonical affine result) does not.
+// Measured (profiles/r04_sortone_runsum_shoup_ab.jsonl, one box, interleaved): 2^12 proofs
+// 7.48 / 7.84 against 7.05 / 7.45 M constraints/s with PLK_SORT_ONE=0.
+constexpr uint32_t kSortOneMax = 8192;
+__global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, uint64_t n_srs,
+                                                   uint32_t chunk, uint32_t* __restrict__ sorted,
+                                                   uint64_t sorted_stride,
+                                                   uint32_t* __restrict__ offsets,
+                                                   uint32_t* __restrict__ task_off,
+                                                   uint2* __restrict__ tasks, uint64_t task_stride,
+                                                   uint32_t* __restrict__ flag, uint32_t gen) {
+  __shared__ uint32_t s_count[kSortSmallMax];
+  __shared__ uint32_t s_c[1024], s_t[1024], s_f[1024], s_len[kChunkMax], s_cur[kChunkMax];
+  const uint32_t slot = blockIdx.y, tid = threadIdx.x, nt = blockDim.x, B = cfg.B;
+  const uint32_t len = batch.len[slot];
+  const Fr* sc = batch.scalars[slot];
+  offsets += (size_t)slot * (B + 1);
+  task_off += (size_t)slot * (B + 1);
+  tasks += (size_t)slot * task_stride;
+  uint32_t* out = sorted + (size_t)slot * sorted_stride;
+  // the commit's degree check (k_any_nonzero): a nonzero scalar in [len, check_len)
+  for (uint64_t i = (uint64_t)len + tid; i < batch.check_len[slot]; i += nt)
+    if (!fe_is_zero(ld_fr(&sc[i]))) atomicMax(&flag[slot], gen);
+  for (uint32_t b = tid; b < B; b += nt) s_count[b] = 0;
+  for (uint32_t l = tid; l < kChunkMax; l += nt) s_len[l] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < len; i += nt) {  // histogram of every digit of the slot
+    bool neg;
+    const Fr s = scalar_half(&sc[i], neg);
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) {
+      const int d = digit_at(s, w, cfg.c, carry);
+      if (d != 0) atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
+    }
+  }
+  __syncthreads();
+  // offsets / task offsets / full-task offsets over each thread's contiguous buckets, the
+  // task records (k_sort_small); s_count[b] becomes bucket b's scatter cursor
+  const uint32_t per = (B + nt - 1) / nt;
+  const uint32_t b0 = min(tid * per, B), b1 = min(b0 + per, B);
+  uint32_t c_sum = 0, t_sum = 0, f_sum = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = s_count[b];
+    c_sum += c;
+    t_sum += (c + chunk - 1) / chunk;
+    f_sum += c / chunk;
+    if (c % chunk) atomicAdd(&s_len[c % chunk], 1u);
+  }
+  s_c[tid] = c_sum;
+  s_t[tid] = t_sum;
+  s_f[tid] = f_sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < nt; off <<= 1) {
+    const uint32_t a = tid >= off ? s_c[tid - off] : 0, t = tid >= off ? s_t[tid - off] : 0;
+    const uint32_t f = tid >= off ? s_f[tid - off] : 0;
+    __syncthreads();
+    s_c[tid] += a;
+    s_t[tid] += t;
+    s_f[tid] += f;
+    __syncthreads();
+  }
+  if (tid == 0) {  // tails after the full tasks, longest first
+    uint32_t run = s_f[nt - 1];
+    for (uint32_t l = chunk - 1; l >= 1; --l) {
+      s_cur[l] = run;
+      run += s_len[l];
+    }
+    offsets[B] = s_c[nt - 1];
+    task_off[B] = s_t[nt - 1];
+  }
+  __syncthreads();
+  uint32_t c_run = s_c[tid] - c_sum, t_run = s_t[tid] - t_sum, f_run = s_f[tid] - f_sum;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t cnt = s_count[b];
+    s_count[b] = c_run;
+    offsets[b] = c_run;
+    task_off[b] = t_run;
+    const uint32_t nfull = cnt / chunk, tail = cnt - nfull * chunk;
+    for (uint32_t t = 0; t < nfull; ++t)
+      tasks[f_run + t] = make_uint2(c_run + t * chunk, (t_run + t) | ((chunk - 1) << kTaskShift));
+    if (tail)
+      tasks[atomicAdd(&s_cur[tail], 1u)] =
+          make_uint2(c_run + nfull * chunk, (t_run + nfull) | ((tail - 1) << kTaskShift));
+    c_run += cnt;
+    t_run += (cnt + chunk - 1) / chunk;
+    f_run += nfull;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < len; i += nt) {  // scatter (k_scatter, one workgroup)
+    bool neg;
+    const Fr s = scalar_half(&sc[i], neg);
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) {
+      const int d = digit_at(s, w, cfg.c, carry);
+      if (d != 0) {
+        const uint32_t pos = atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
+        out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
+      }
+    }
+  }
+}
+
 // ---- wide bucket sets (B > kLdsBuckets, c >= 17): two-level radix sort ----------------
 // One LDS histogram cannot hold the buckets, and per-(workgroup, bucket) runs of ~1 entry
 // make a direct scatter write-amplified. Instead: (1) coarse bins of kFine consecutive
@@ -1213,7 +1322,12 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     w.gen = 1;
   }
   const uint32_t gen = w.gen;
-  if (max_tail) {
+  // small batches: the whole sort (and the degree check) in one dispatch per batch
+#ifndef PLK_SORT_ONE
+#define PLK_SORT_ONE 1
+#endif
+  const bool sort_one = PLK_SORT_ONE && !wide && B <= kSortSmallMax && max_len <= kSortOneMax;
+  if (max_tail && !sort_one) {
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
                        batch, hdr_dev->flag, gen);
   }
@@ -1244,6 +1358,11 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        (const uint32_t*)w.bin_tot.as<uint32_t>(),
                        (const uint32_t*)w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>(),
                        w.task_off.as<uint32_t>(), w.tasks.as<uint2>(), (uint64_t)w.task_stride);
+  } else if (sort_one) {
+    hipLaunchKernelGGL(k_sort_one, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
+                       (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
+                       w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
+                       (uint64_t)w.task_stride, hdr_dev->flag, gen);
   } else {
     const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
     if (max_len) {

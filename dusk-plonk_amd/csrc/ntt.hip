@@ -239,6 +239,13 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
 // Products by the inner (stage) twiddles staged in LDS. PLK_NTT_SHOUP: the table holds
 // (w, w' = floor(w 2^261 / r)) planes and the product is the constant-operand Shoup form
 // (ffr.hpp fr_shoup, 143 mads, output < 3r); otherwise Montgomery by w R' (rx_mul, < 2r).
+// Measured (round 4, profiles/r04_sortone_runsum_shoup_ab.jsonl, parity-green with the NTT
+// and prover tests): dft + idft per step 2^20 0.310-0.313 against 0.298-0.302 ms, 2^23
+// 2.171-2.174 against 2.097-2.121 ms — SLOWER. As compiled, the last low column's 18 products
+// become v_mul_lo_u32 (only their low bits count), the small constants of 2^261 - r become
+// multiply / shift sequences and LLVM splits the chains with 64-bit merge adds: 472 mads +
+// 96 v_mul_lo_u32 against 612 mads, the same VALU cycles per loop body, and a standalone
+// product rate 1.15-1.25e11 against 1.31-1.40e11 /s (tools/ubench_shoup.hip). Off.
 #ifndef PLK_NTT_SHOUP
 #define PLK_NTT_SHOUP 0
 #endif

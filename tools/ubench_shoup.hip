@@ -24,25 +24,23 @@ using RFr = Rx<FrCfg>;
     }                                                                               \
   } while (0)
 
-// (w, w') of a canonical R'-domain twiddle rho = w R' mod r
-__global__ void k_prep(const Fr* rho, Fr* w, Fr* wp, uint32_t n) {
+// (w, w') of a canonical R'-domain twiddle rho = w R' mod r, kept as raw limbs (w' is a
+// 261-bit value: it does not fit the packed 256-bit layout)
+__global__ void k_prep(const Fr* rho, RFr* w, RFr* wp, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  RFr a, b;
-  fr_shoup_prep(rx_unpack(rho[i]), a, b);
-  w[i] = rx_pack(a);
-  wp[i] = rx_pack(b);
+  fr_shoup_prep(rx_unpack(rho[i]), w[i], wp[i]);
 }
 
 // out = x * w mod r (canonical) both ways; mode 1: x -> x + 6r - y (unnormalised limbs)
-__global__ void k_check(const Fr* x, const Fr* y, const Fr* rho, const Fr* w, const Fr* wp,
+__global__ void k_check(const Fr* x, const Fr* y, const Fr* rho, const RFr* w, const RFr* wp,
                         uint32_t n, int mode, uint32_t* bad) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   RFr a = rx_unpack(x[i]);
   if (mode == 1) a = rx_sub_u<FrCfg, 6>(a, rx_unpack(y[i]));
   const Fr m = rx_pack_canonical(rx_mul(a, rx_unpack(rho[i])));
-  Fr s = rx_pack(fr_shoup(a, rx_unpack(w[i]), rx_unpack(wp[i])));  // [0, 3r)
+  Fr s = rx_pack(fr_shoup(a, w[i], wp[i]));  // [0, 3r)
   fe_reduce_once(s);
   fe_reduce_once(s);
   for (int k = 0; k < 8; ++k)
@@ -53,15 +51,15 @@ __global__ void k_check(const Fr* x, const Fr* y, const Fr* rho, const Fr* w, co
 }
 
 template <int FORM>
-__global__ void __launch_bounds__(256) k_thr(Fr* io, const Fr* rho, const Fr* w, const Fr* wp,
+__global__ void __launch_bounds__(256) k_thr(Fr* io, const Fr* rho, const RFr* w, const RFr* wp,
                                              uint32_t iters) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   RFr x0 = rx_unpack(io[2 * i]), x1 = rx_unpack(io[2 * i + 1]);
   RFr c[4], cp[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    c[k] = rx_unpack(FORM == 0 ? rho[k] : w[k]);
-    cp[k] = rx_unpack(wp[k]);
+    c[k] = FORM == 0 ? rx_unpack(rho[k]) : w[k];
+    cp[k] = wp[k];
   }
   for (uint32_t it = 0; it < iters; ++it) {
 #pragma unroll
@@ -109,13 +107,14 @@ int main() {
     hx[1].v[k] = FrCfg::P[k];
   }
   hx[1].v[0] -= 1;
-  Fr *dx, *dy, *drho, *dw, *dwp;
+  Fr *dx, *dy, *drho;
+  RFr *dw, *dwp;
   uint32_t* dbad;
   CHECK(hipMalloc(&dx, n * sizeof(Fr)));
   CHECK(hipMalloc(&dy, n * sizeof(Fr)));
   CHECK(hipMalloc(&drho, n * sizeof(Fr)));
-  CHECK(hipMalloc(&dw, n * sizeof(Fr)));
-  CHECK(hipMalloc(&dwp, n * sizeof(Fr)));
+  CHECK(hipMalloc(&dw, n * sizeof(RFr)));
+  CHECK(hipMalloc(&dwp, n * sizeof(RFr)));
   CHECK(hipMalloc(&dbad, 4));
   CHECK(hipMemcpy(dx, hx.data(), n * sizeof(Fr), hipMemcpyHostToDevice));
   CHECK(hipMemcpy(dy, hy.data(), n * sizeof(Fr), hipMemcpyHostToDevice));
