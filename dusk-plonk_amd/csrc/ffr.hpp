@@ -95,9 +95,10 @@ struct RxK {
 
 // Split-column plan of a Montgomery product with NPROD operand products (1: a*b or a^2,
 // 2: a*b + c*d) for shapes whose columns can overflow 64 bits (B >= 30). Operand limbs are
-// normalised (< 2^B) with a top limb below 2^(TOP_BITS) (values below 2^(B(L-1) + TOP_BITS):
-// every operand of the group law stays below 40p < 2^386, and the products' output bound
-// a b / R' + p < 2p already needs a b < 630 p^2 at R' = 2^390). split[k]: the worst-case sum
+// normalised (< 2^B) with a top limb below 2^(TOP_BITS) (values below 2^(B(L-1) + TOP_BITS)
+// = 2^386 for Fp): the group-law operands stay below 12p (~2^384.3; rx_sub_u<10> of two
+// values < 2p is the largest), checked by the static_assert below the plan; the products'
+// output bound a b / R' + p < 2p also needs a b < 630 p^2 at R' = 2^390. split[k]: the worst-case sum
 // of column k (incoming carry + products + reduction terms m_i p_j) reaches 2^64, so the
 // products and the reduction terms (and for NPROD = 2 each product set) use separate
 // accumulators there. Every separate accumulator holds at most L products below 2^60 plus
@@ -133,6 +134,7 @@ template <class C, int NPROD>
 struct RxPlanK {
   static constexpr RxPlan<C, NPROD> k{};
 };
+// (defined below) the limbs of c*p
 // c*p as L limbs (c < 16). borrow_free: every limb below the top raised by 2^B - 1 (2^B for
 // limb 0) by borrowing from the limb above, so limbs 0..L-2 lie in [2^B - 1, 2^(B+1) - 1):
 // a_i + q_i - b_i >= 0 limb by limb for any normalised b whose top limb is below q's.
@@ -166,6 +168,12 @@ template <class C, uint32_t CP, bool BF>
 struct RxMultipleK {
   static constexpr RxMultiple<C> k = rx_multiple<C>(CP, BF);
 };
+// The split plan's operand bound: the largest group-law multiplicand (below 12p, e.g.
+// rx_sub_u<10>(a, b) with a < 2p) must keep its top limb below 2^TOP_BITS, or a column the plan
+// leaves unsplit could reach 2^64. A looser operand bound must update TOP_BITS (and the plan).
+static_assert(RxMultiple<FpCfg>{rx_multiple<FpCfg>(12, false)}.v[RxShape<FpCfg>::L - 1] <
+                  (1u << RxPlan<FpCfg, 1>::TOP_BITS),
+              "12p exceeds the split plan's operand bound");
 
 #define PLK_RX __device__ __forceinline__
 
@@ -756,13 +764,16 @@ PLK_RX bool rx_maybe_multiple(uint32_t a0, uint32_t b0, uint32_t kpos, uint32_t 
   return (((a0 - b0) * K.inv + kpos) & MASK) <= kpos + kneg;
 }
 
-// a (any value < 16p, limbs < 2^(B+2)) reduced to [0, 2p), normalised: a * R' / R'
+// a reduced to [0, 2p), normalised: a * R' / R'. Operands: for unsplit shapes (Fr) any value
+// < 16p with limbs < 2^(B+2); for split shapes (Fp 13 x 30) normalised limbs (< 2^B) and a
+// value within the split plan's bound (< 12p, RxPlan).
 template <class C>
 PLK_RX Rx<C> rx_canon(const Rx<C>& a) {
   return rx_mul(a, rx_one<C>());
 }
 
-// a == 0 mod p for a value < 16p with limbs < 2^(B+2): (a / R') is in [0, 2p)
+// a == 0 mod p, operands as rx_canon's (unsplit shapes: < 16p, limbs < 2^(B+2); split
+// shapes: normalised limbs, < 12p): (a / R') is in [0, 2p)
 template <class C>
 PLK_RX bool rx_is_zero_u(const Rx<C>& a) {
   Rx<C> one = rx_zero<C>();
