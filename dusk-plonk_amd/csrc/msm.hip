@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
                                                    uint32_t* __restrict__ flag, uint32_t gen) {
   __shared__ uint32_t s_count[kSortSmallMax];
   __shared__ uint32_t s_c[1024], s_t[1024], s_f[1024], s_len[kChunkMax], s_cur[kChunkMax];
-  const uint32_t slot = blockIdx.y, tid = threadIdx.x, nt = blockDim.x, B = cfg.B;
+  const uint32_t slot = blockIdx.y, tid = threadIdx.x, nt = 1024, B = cfg.B;  // blockDim.x
   const uint32_t len = batch.len[slot];
   const Fr* sc = batch.scalars[slot];
   offsets += (size_t)slot * (B + 1);
@@ -434,12 +434,23 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   for (uint32_t b = tid; b < B; b += nt) s_count[b] = 0;
   for (uint32_t l = tid; l < kChunkMax; l += nt) s_len[l] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < len; i += nt) {  // histogram of every digit of the slot
-    bool neg;
-    const Fr s = scalar_half(&sc[i], neg);
+  // this thread's scalars (i = tid + k nt, at most kSortOneMax / 1024 of them), brought to
+  // [0, (r-1)/2] once and kept in registers for both passes
+  constexpr uint32_t kPer = kSortOneMax / 1024;
+  Fr sv[kPer];
+  bool sneg[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = tid + k * nt;
+    sneg[k] = false;
+    if (i < len) sv[k] = scalar_half(&sc[i], sneg[k]);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {  // histogram of every digit of the slot
+    if (tid + k * nt >= len) break;
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg.c, carry);
+      const int d = digit_at(sv[k], w, cfg.c, carry);
       if (d != 0) atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
     }
   }
@@ -496,15 +507,16 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
     f_run += nfull;
   }
   __syncthreads();
-  for (uint32_t i = tid; i < len; i += nt) {  // scatter (k_scatter, one workgroup)
-    bool neg;
-    const Fr s = scalar_half(&sc[i], neg);
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter, one workgroup)
+    const uint32_t i = tid + k * nt;
+    if (i >= len) break;
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg.c, carry);
+      const int d = digit_at(sv[k], w, cfg.c, carry);
       if (d != 0) {
         const uint32_t pos = atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
-        out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
+        out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != sneg[k]) ? 0x80000000u : 0u);
       }
     }
   }
@@ -1209,7 +1221,9 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
   const size_t max_runs = std::max<size_t>(slots * (B >> kRunBits), B >> kRunBitsMin);
   if (wide && NC > kCoarseMax) return PLK_E_ARG;
   const size_t entries = (size_t)s->windows * len;
-  const size_t max_tasks = entries / kChunkMin + B + 1;
+  // small shapes (k_sort_one's) may run tasks of kChunkSmall points (msm_run_batch)
+  const uint32_t chunk_min = (!wide && B <= kSortSmallMax && len <= kSortOneMax) ? kChunkSmall : kChunkMin;
+  const size_t max_tasks = entries / chunk_min + B + 1;
   const size_t groups = wide ? (max_runs + 255) / 256 : slots * ((B + 255) / 256);
   if (max_tasks >= ((size_t)1 << kTaskShift)) return PLK_E_ARG;  // task records: partial index bits
   int st;
@@ -1259,6 +1273,7 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   w.cap_len = len;
   w.cap_slots = slots;
+  w.cap_chunk_min = chunk_min;
   w.cap_c = s->c;
   w.cap_windows = s->windows;
   w.task_stride = max_tasks;
@@ -1305,10 +1320,14 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   // A lone wide MSM below ~2^18 points (configs[2]-style commits at 2^16) would leave one
   // task of ~15-35 dependent additions per bucket on a half-empty chip: it takes the chunk
   // formula too (16 at 2^16, 52 at 2^20)
+  const bool small_batch = !wide && B <= kSortSmallMax && max_len <= kSortOneMax;
+  // the task-length floor: kChunkSmall for small batches when the workspace was sized for it
+  const uint32_t chunk_floor = small_batch ? std::max(kChunkSmall, w.cap_chunk_min) : kChunkMin;
   const uint32_t chunk_fit =
-      (uint32_t)std::min<size_t>(kChunkMax, std::max<size_t>(kChunkMin, total_entries / PLK_CHUNK_TARGET));
+      (uint32_t)std::min<size_t>(kChunkMax, std::max<size_t>(chunk_floor, total_entries / PLK_CHUNK_TARGET));
   const uint32_t chunk = wide && count > 1 ? kChunkMax : chunk_fit;
   const size_t max_tasks_used = (size_t)s->windows * max_len / chunk + B;
+  if (max_tasks_used + 1 > w.task_stride) return PLK_E_DEVICE;  // sizing invariant (ws_reserve)
   // 256 workgroups per slot: fewer give longer per-bucket write runs in k_scatter but lose
   // more parallelism than they gain (measured 2.77 / 2.79 / 3.02 / 4.52 ms per proof at
   // 256 / 128 / 64 / 32, tools/gpu_hist_sweep.sh)
@@ -1326,7 +1345,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
 #ifndef PLK_SORT_ONE
 #define PLK_SORT_ONE 1
 #endif
-  const bool sort_one = PLK_SORT_ONE && !wide && B <= kSortSmallMax && max_len <= kSortOneMax;
+  const bool sort_one = PLK_SORT_ONE && small_batch;
   if (max_tail && !sort_one) {
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
                        batch, hdr_dev->flag, gen);

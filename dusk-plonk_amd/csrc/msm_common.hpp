@@ -7,7 +7,17 @@ namespace plk {
 #ifndef PLK_CHUNK_MAX
 #define PLK_CHUNK_MAX 64
 #endif
-constexpr uint32_t kChunkMin = 16;  // points per accumulation task (bounds)
+#ifndef PLK_CHUNK_MIN
+#define PLK_CHUNK_MIN 16
+#endif
+constexpr uint32_t kChunkMin = PLK_CHUNK_MIN;  // points per accumulation task (bounds)
+// small batches (the one-dispatch sort's: B <= 4 096, <= 8 192 scalars per slot) take tasks
+// of down to 8 points: their latency-bound accumulation chains halve (round 4: 2^12 proofs
+// +7 %; 8 everywhere cost the 2^14 / 2^16 proofs and the lone 2^16 MSM 1-3 %)
+#ifndef PLK_CHUNK_SMALL
+#define PLK_CHUNK_SMALL 8
+#endif
+constexpr uint32_t kChunkSmall = PLK_CHUNK_SMALL;
 constexpr uint32_t kChunkMax = PLK_CHUNK_MAX;
 // task record .y = partial index | (length - 1) << kTaskShift
 constexpr uint32_t kTaskShift = 32 - (kChunkMax <= 64 ? 6 : 7);
@@ -97,6 +107,7 @@ struct MsmWorkspace {
   // (a prover's key SRS, then a shard slice with another window size), and every size
   // above depends on c and the window count
   uint32_t cap_c = 0, cap_windows = 0;
+  uint32_t cap_chunk_min = kChunkMin;  // the task-length floor the buffers were sized for
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   MsmStats stats;
   ~MsmWorkspace() {
