@@ -138,7 +138,9 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
 __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, const RFp& y2) {
 #if PLK_MADD_GROUPED
   // the same nine reductions as independent groups whose chains interleave (ffr.hpp
-  // rx_prod_group): (U2, S2), (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3)
+  // rx_prod_group): (U2, S2), (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3). (PPP, Q, ZZ3) then
+  // (Y3, ZZZ3) compiled to 402 instead of 536 s_nop but issued at the same rate (6.58-6.61e9
+  // against 6.56-6.62e9 additions/s, profiles/r04_madd_grouping_ab.txt): not kept.
   RFp U2, S2, PP, RR, PPP, Q;
   rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
   const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
@@ -290,6 +292,84 @@ __device__ __forceinline__ G1R g1r_add_lazy_fix(const G1R& p, const G1R& q, cons
 __device__ __forceinline__ G1R g1r_add_lazy(const G1R& p, const G1R& q) {
   const G1R r = g1r_add_lazy_sl(p, q);
   return rx_is_zero(r.ZZ) ? g1r_add_lazy_fix(p, q, r.X) : r;  // rare branch
+}
+
+// ---- quad-cooperative lazy full addition, for the latency-bound reduction tails -------
+// One addition per quad (4 consecutive lanes holding the same p and q; the result comes
+// back in all four). A lone wave's addition is issue-bound: g1r_add_lazy_sl issues ~15
+// Montgomery products one after another. Here the quad's lanes take one product each in
+// the same instruction stream, four levels of the formula's dependency graph:
+//   1: U1 = X1 ZZ2, U2 = X2 ZZ1, S1 = Y1 ZZZ2, S2 = Y2 ZZZ1
+//   2: PP = P^2, RR = R^2, ZZ1 ZZ2, ZZZ1 ZZZ2       (P = U2 - U1, R = S2 - S1)
+//   3: PPP = P PP, Q = U1 PP, ZZ3 = ZZ1 ZZ2 PP
+//   4: Y3 = R (Q - X3) + (5p - S1) PPP, ZZZ3 = ZZZ1 ZZZ2 PPP   (one fused form, c d = 0 on
+//      the ZZZ3 lane)
+// and the lanes swap results through DPP quad broadcasts: ~3.5 products issued instead of ~15.
+// Same formulas and bounds as g1r_add_lazy_sl (each lane selects its level's operands from the
+// same values); squares run as products. The quad must be active as a whole (control flow
+// uniform per quad). Measured (profiles/r04_tail_quad_ab.jsonl): lone MSMs 2^16 0.82 -> 0.68 ms,
+// 2^20 3.30 -> 3.01-3.10 ms; 2^12 proofs +8-15 %; proofs at 2^16 / 2^20, where other lanes'
+// kernels fill the chip, ~1 % slower (more issue slots per addition): prover lanes above
+// 2^14 keep the single-lane trees (msm_common.hpp tail_quad).
+template <int K>
+__device__ __forceinline__ RFp quad_bcast(const RFp& v) {
+  RFp r;
+#pragma unroll
+  for (int i = 0; i < RxShape<FpCfg>::L; ++i)
+    r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], K | (K << 2) | (K << 4) | (K << 6), 0xF,
+                                                0xF, false);
+  return r;
+}
+
+__device__ __forceinline__ RFp quad_sel(uint32_t l, const RFp& a0, const RFp& a1, const RFp& a2,
+                                        const RFp& a3) {
+  RFp r;
+#pragma unroll
+  for (int i = 0; i < RxShape<FpCfg>::L; ++i)
+    r.v[i] = l < 2 ? (l == 0 ? a0.v[i] : a1.v[i]) : (l == 2 ? a2.v[i] : a3.v[i]);
+  return r;
+}
+
+// Operands as for g1r_add_lazy. Infinity operands return early (uniform per quad); the
+// equal-x case is repaired from (U1, S1, ZZ1 ZZ2, ZZZ1 ZZZ2), which represents p itself
+// (p scaled by ZZ2: U1 / ZZ12 = X1 / ZZ1, S1 / ZZZ12 = Y1 / ZZZ1), so neither operand stays
+// live past level 2.
+__device__ __forceinline__ G1R g1r_add_quad(const G1R& p, const G1R& q, uint32_t l) {
+  if (g1r_is_inf(q)) return p;
+  if (g1r_is_inf(p)) return q;
+  RFp M = rx_mul(quad_sel(l, p.X, q.X, p.Y, q.Y), quad_sel(l, q.ZZ, p.ZZ, q.ZZZ, p.ZZZ));
+  const RFp U1 = quad_bcast<0>(M), S1 = quad_bcast<2>(M);
+  const RFp P = rx_sub_u<FpCfg, 3>(quad_bcast<1>(M), U1);  // U2 - U1 + 3p in (p, 5p)
+  const RFp R = rx_sub_u<FpCfg, 3>(quad_bcast<3>(M), S1);  // S2 - S1 + 3p in (p, 5p)
+  M = rx_mul(quad_sel(l, P, R, p.ZZ, p.ZZZ), quad_sel(l, P, R, q.ZZ, q.ZZZ));
+  const RFp PP = quad_bcast<0>(M), RR = quad_bcast<1>(M), ZZ12 = quad_bcast<2>(M),
+            ZZZ12 = quad_bcast<3>(M);
+  M = rx_mul(quad_sel(l, P, U1, ZZ12, ZZ12), PP);
+  const RFp PPP = quad_bcast<0>(M), Q = quad_bcast<1>(M);
+  G1R r;
+  r.ZZ = quad_bcast<2>(M);
+  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
+  if (rx_is_zero(r.ZZ)) {  // P = 0 (rare): the doubling of p if R = 0 (then X3 = R^2 + 6p), else infinity
+    uint32_t z = 0;
+    __asm__ volatile(";; plk rare path" : "+v"(z));  // as in g1r_add_lazy_fix
+    RFp x = r.X;
+    x.v[0] += z;
+    if (!rx_is_zero_u(x)) return g1r_infinity();
+    G1R d;
+    d.X = U1;
+    d.Y = S1;
+    d.ZZ = ZZ12;
+    d.ZZZ = ZZZ12;
+    d.X.v[0] += z;
+    return g1r_dbl_lazy(d);
+  }
+  const RFp qx = rx_sub_u<FpCfg, 10>(Q, r.X), cd = rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), S1);
+  const RFp z = rx_zero<FpCfg>();
+  M = rx_mul_add(quad_sel(l, R, ZZZ12, R, ZZZ12), quad_sel(l, qx, PPP, qx, PPP),
+                 quad_sel(l, cd, z, cd, z), PPP);
+  r.Y = quad_bcast<0>(M);
+  r.ZZZ = quad_bcast<1>(M);
+  return r;
 }
 
 // ---- packed memory <-> limbs (16-byte loads/stores of the 48-byte coordinates) -------

@@ -898,6 +898,35 @@ __device__ __forceinline__ G1R shfl_tree(G1R acc, uint32_t e, uint32_t w) {
   return acc;
 }
 
+// QUAD (PLK_BITSUM_QUAD): every "lane" of the reduction trees (k_bucket_sum, k_bitsum1/2) is a quad of 4 lanes holding the same
+// values, adding with g1r_add_quad (g1r.hpp: one product per lane, ~3.5 products issued per
+// addition instead of ~15) — these trees are a chain of dependent additions on a few waves,
+// so their time is one wave's issue of each level. Shuffles move by whole quads.
+#ifndef PLK_BITSUM_QUAD
+#define PLK_BITSUM_QUAD 1
+#endif
+template <bool QUAD>
+struct TailUnit {
+  static constexpr uint32_t S = QUAD ? 4 : 1;  // lanes per unit
+  uint32_t u, l;                               // unit index, lane in the unit
+  __device__ explicit TailUnit(uint32_t tid) : u(tid / S), l(tid % S) {}
+  template <bool LAZY>
+  __device__ __forceinline__ G1R add(const G1R& a, const G1R& b) const {
+    if constexpr (QUAD) return g1r_add_quad(a, b, l);
+    else return g1r_add_t<LAZY>(a, b);
+  }
+  __device__ __forceinline__ G1R down(const G1R& v, uint32_t h) const { return shfl_down_g1r(v, h * S); }
+  // sum over groups of w consecutive units (aligned, inside one wave), e = unit in the group
+  template <bool LAZY>
+  __device__ __forceinline__ G1R tree(G1R acc, uint32_t e, uint32_t w) const {
+    for (uint32_t h = w >> 1; h >= 1; h >>= 1) {
+      const G1R o = down(acc, h);
+      if (e < h) acc = add<LAZY>(acc, o);
+    }
+    return acc;
+  }
+};
+
 // k_bitsum1: the branching addition at two waves per SIMD (2 workgroups of 256 per CU: a lone
 // 2^20 MSM's 512 groups in one round instead of two)
 #ifndef PLK_BITSUM_LAZY
@@ -907,24 +936,23 @@ __device__ __forceinline__ G1R shfl_tree(G1R acc, uint32_t e, uint32_t w) {
 #define PLK_BITSUM_WAVES 2
 #endif
 
+template <bool QUAD>
 __global__ void __launch_bounds__(256) k_bucket_sum(const uint32_t* __restrict__ task_off,
                                                     uint32_t B, uint32_t lp, uint64_t task_stride,
                                                     const G1xyzz* __restrict__ partials,
                                                     G1xyzz* __restrict__ bsum) {
-  const uint32_t slot = blockIdx.y, tid = threadIdx.x;
-  const uint32_t P = 1u << lp, s = tid & (P - 1);
-  const uint32_t b = (blockIdx.x * 256 + tid) >> lp;
+  const uint32_t slot = blockIdx.y;
+  const TailUnit<QUAD> T(blockIdx.x * 256 + threadIdx.x);  // unit = one lane of the bucket's 2^lp
+  const uint32_t P = 1u << lp, s = T.u & (P - 1);
+  const uint32_t b = T.u >> lp;
   task_off += (size_t)slot * (B + 1);
   partials += (size_t)slot * task_stride;
   // the branching g1r_add here: ~200 VGPRs (2 waves per SIMD) against ~325 for the lazy form
   G1R acc = g1r_infinity();
   if (b < B)
-    for (uint32_t t = task_off[b] + s; t < task_off[b + 1]; t += P) acc = g1r_add(acc, ld_g1r(&partials[t]));
-  for (uint32_t h = P >> 1; h >= 1; h >>= 1) {  // lanes s < h add lane s + h (same bucket)
-    const G1R o = shfl_down_g1r(acc, h);
-    if (s < h) acc = g1r_add(acc, o);
-  }
-  if (s == 0 && b < B) st_g1r(&bsum[(size_t)slot * B + b], acc);
+    for (uint32_t t = task_off[b] + s; t < task_off[b + 1]; t += P) acc = T.template add<false>(acc, ld_g1r(&partials[t]));
+  acc = T.template tree<false>(acc, s, P);  // units s < h add unit s + h (same bucket)
+  if (s == 0 && T.l == 0 && b < B) st_g1r(&bsum[(size_t)slot * B + b], QUAD ? g1r_lazy_finish(acc) : acc);
 }
 
 #ifndef PLK_RUNSUM_WAVES
@@ -1023,8 +1051,14 @@ __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
   return ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
 }
 
-template <bool Z>
-__global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
+// threads of k_bitsum1: 4 units per row / column sum, 1 or 4 lanes per unit; quads with Z
+// take 2 units per sum (8 members each), so a workgroup stays at 8 waves (2 per SIMD: the quad
+// addition needs ~250 VGPRs)
+constexpr uint32_t bitsum1_threads(bool z, bool quad) {
+  return quad ? (z ? 384 : 512) : (z ? 192 : 128);
+}
+template <bool Z, bool QUAD>
+__global__ void __launch_bounds__(bitsum1_threads(Z, QUAD), PLK_BITSUM_WAVES) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
                                                                            const G1xyzz* __restrict__ zin,
                                                                            G1xyzz* __restrict__ out,
                                                                            BitsumFold fold) {
@@ -1032,15 +1066,19 @@ __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uin
   // read straight from HBM and the trees run over cross-lane shuffles: LDS holds only the
   // NS row / column sums (9 KiB instead of 105 — a resident k_bitsum1 used to keep the other
   // proofs' NTT passes off its CU).
-  // The NS sums of 16 take 4 consecutive lanes each, and each lane first adds its 4 members
-  // in sequence (every lane busy), then a 2-level shuffle tree: 3 + 2 levels on NS / 16 waves.
+  // The NS sums of 16 take 4 consecutive units each, and each unit first adds its 4 members
+  // in sequence (every unit busy), then a 2-level shuffle tree: 3 + 2 levels on NS / 16 waves.
   // The tree kernels are issue-bound — a wave issues the whole addition however few of its
-  // lanes are active — so lanes idle in a shuffle level cost as much as busy ones: 8 lanes
+  // lanes are active — so units idle in a shuffle level cost as much as busy ones: 8 units
   // per sum with 2 members each (3-level tree) issued twice the wave-additions (round 3:
   // 8 waves x 4 levels + 4 against 3 waves x 5 levels + 4 per group).
   constexpr uint32_t NS = Z ? 48 : 32;
+  constexpr uint32_t NSU = (QUAD && Z) ? 2 : 4, MEM = 16 / NSU;  // units per sum, members per unit
+  constexpr uint32_t NU = bitsum1_threads(Z, QUAD) / TailUnit<QUAD>::S;  // units
+  constexpr bool LZ = PLK_BITSUM_LAZY;
   __shared__ G1xyzz sh[NS];
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  const TailUnit<QUAD> T(tid);
   out += ((size_t)slot * gridDim.x + g) * kBitsumOut;
   auto value = [&](uint32_t x) -> G1R {  // x < 256: bsum, else zin; past B: infinity
     const uint32_t b = g * 256 + (x & 255);
@@ -1048,25 +1086,27 @@ __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uin
     return b < B ? ld_g1r(&src[(size_t)slot * B + b]) : g1r_infinity();
   };
   {  // sum q < 16: row a = q (members 16q + c); 16 <= q < 32: column c = q - 16 (members
-     // c + 16a); q >= 32 (Z): row q - 32 of the plain-sum values. Lane e < 4 of the sum's 4
-     // takes members 4e .. 4e + 3 of its row / column.
-    const uint32_t q = tid >> 2, e = tid & 3;
+     // c + 16a); q >= 32 (Z): row q - 32 of the plain-sum values. Unit e < NSU of the sum's
+     // NSU takes members MEM e .. MEM e + MEM - 1 of its row / column.
+    const uint32_t q = T.u / NSU, e = T.u % NSU;
     auto member = [&](uint32_t i) {  // i-th member of sum q, i < 16
       return q < 16 ? 16 * q + i : q < 32 ? (q - 16) + 16 * i : 256 + 16 * (q - 32) + i;
     };
-    G1R acc = value(member(4 * e));
+    G1R acc = value(member(MEM * e));
 #pragma unroll 1
-    for (uint32_t i = 1; i < 4; ++i) acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, value(member(4 * e + i)));
-    acc = shfl_tree<PLK_BITSUM_LAZY>(acc, e, 4);
-    if (e == 0) st_g1r(&sh[q], acc);
+    for (uint32_t i = 1; i < MEM; ++i) acc = T.template add<LZ>(acc, value(member(MEM * e + i)));
+    acc = T.template tree<LZ>(acc, e, NSU);
+    if (e == 0 && T.l == 0) st_g1r(&sh[q], acc);
   }
   __syncthreads();
-  // wave 0: lanes 0..31 = T_0..T_7, 4 lanes each (2 terms per lane); lanes 32..39 = A_g, 8 lanes
-  // (rows 2e, 2e + 1); with Z lanes 40..47 = the plain sum (its rows 2e, 2e + 1); then trees
-  if (tid < 64) {
-    const bool on = tid < (Z ? 48u : 40u);
-    const uint32_t s = tid < 32 ? tid >> 2 : tid < 40 ? 8 : 9, e = tid < 32 ? tid & 3 : (tid - 32) & 7;
-    const uint32_t w = tid < 32 ? 4 : 8;
+  // units 0..31 = T_0..T_7, 4 units each (2 terms per unit); units 32..39 = A_g, 8 units
+  // (rows 2e, 2e + 1); with Z units 40..47 = the plain sum (its rows 2e, 2e + 1); then trees
+  // (unit groups never straddle a wave: 4 or 8 units of 1 or 4 lanes, aligned)
+  if (T.u < 64) {
+    const uint32_t t = T.u;
+    const bool on = t < (Z ? 48u : 40u);
+    const uint32_t s = t < 32 ? t >> 2 : t < 40 ? 8 : 9, e = t < 32 ? t & 3 : (t - 32) & 7;
+    const uint32_t w = t < 32 ? 4 : 8;
     uint32_t i0 = 0, i1 = 0;
     if (s < 4) {  // columns c with bit s
       i0 = 16 + with_bit(2 * e, s);
@@ -1078,12 +1118,13 @@ __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uin
       i0 = (s == 8 ? 0 : 32) + 2 * e;
       i1 = i0 + 1;
     }
-    G1R acc = on ? g1r_add_t<PLK_BITSUM_LAZY>(ld_g1r(&sh[i0]), ld_g1r(&sh[i1])) : g1r_infinity();
-    for (uint32_t h = 4; h >= 1; h >>= 1) {  // groups of w consecutive lanes
-      const G1R o = shfl_down_g1r(acc, h);
-      if (on && e < h && h < w) acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, o);
+    G1R acc = g1r_infinity();
+    if (on) acc = T.template add<LZ>(ld_g1r(&sh[i0]), ld_g1r(&sh[i1]));
+    for (uint32_t h = 4; h >= 1; h >>= 1) {  // groups of w consecutive units
+      const G1R o = T.down(acc, h);
+      if (on && e < h && h < w) acc = T.template add<LZ>(acc, o);
     }
-    if (on && e == 0) st_g1r(&out[s], acc);
+    if (on && e == 0 && T.l == 0) st_g1r(&out[s], acc);
   }
   if (!fold.done) return;
   // few groups (G <= kFoldMaxGroups): the slot's last workgroup to finish runs k_bitsum2's sums
@@ -1097,23 +1138,26 @@ __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uin
   if (!s_last) return;
   __threadfence();
   const G1xyzz* in = out - (size_t)g * kBitsumOut;  // this slot's groups
-  const uint32_t j = tid >> 3, e = tid & 7, G = gridDim.x;
-  G1R acc = g1r_infinity();
-  if (j < fold.nout) {  // output j: 8 lanes, lane e takes the groups g = e mod 8
-    for (uint32_t gg = e; gg < G; gg += 8) {
-      const G1xyzz* v = &in[(size_t)gg * kBitsumOut];
-      if (j >= fold.nbits) {  // wide sets: the plain sums (j = nbits) and the A_g (nbits + 1)
-        acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[j == fold.nbits ? 9 : 8]));
-      } else if (j < 8) {
-        acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[j]));
-        if (j == 0) acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[8]));
-      } else if ((gg >> (j - 8)) & 1u) {
-        acc = g1r_add_t<PLK_BITSUM_LAZY>(acc, ld_g1r(&v[8]));
+  const uint32_t e = T.u & 7, G = gridDim.x;
+  for (uint32_t j0 = 0; j0 < fold.nout; j0 += NU / 8) {  // uniform trip count: the trees shuffle
+    const uint32_t j = j0 + (T.u >> 3);
+    G1R acc = g1r_infinity();
+    if (j < fold.nout) {  // output j: 8 units, unit e takes the groups g = e mod 8
+      for (uint32_t gg = e; gg < G; gg += 8) {
+        const G1xyzz* v = &in[(size_t)gg * kBitsumOut];
+        if (j >= fold.nbits) {  // wide sets: the plain sums (j = nbits) and the A_g (nbits + 1)
+          acc = T.template add<LZ>(acc, ld_g1r(&v[j == fold.nbits ? 9 : 8]));
+        } else if (j < 8) {
+          acc = T.template add<LZ>(acc, ld_g1r(&v[j]));
+          if (j == 0) acc = T.template add<LZ>(acc, ld_g1r(&v[8]));
+        } else if ((gg >> (j - 8)) & 1u) {
+          acc = T.template add<LZ>(acc, ld_g1r(&v[8]));
+        }
       }
     }
+    acc = T.template tree<LZ>(acc, e, 8);
+    if (j < fold.nout && e == 0 && T.l == 0) st_g1r(&fold.out2[(size_t)slot * fold.nout + j], g1r_lazy_finish(acc));
   }
-  acc = shfl_tree<PLK_BITSUM_LAZY>(acc, e, 8);
-  if (j < fold.nout && e == 0) st_g1r(&fold.out2[(size_t)slot * fold.nout + j], g1r_lazy_finish(acc));
   if (tid == 0) {
     fold.entries[slot] = fold.offsets[(size_t)slot * (fold.B + 1) + fold.B];
     fold.done[slot] = 0;  // ready for the next batch (stream order)
@@ -1130,21 +1174,27 @@ __global__ void __launch_bounds__(Z ? 192 : 128, PLK_BITSUM_WAVES) k_bitsum1(uin
 #ifndef PLK_BITSUM2_LAZY
 #define PLK_BITSUM2_LAZY 1
 #endif
-__global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
+// QUAD: 128 units of 4 lanes (8 waves, 2 per SIMD: the quad addition's ~250 VGPRs)
+constexpr uint32_t kBitsum2Units(bool quad) { return quad ? 128 : 256; }
+template <bool QUAD>
+__global__ void __launch_bounds__(QUAD ? 512 : 256) k_bitsum2(const G1xyzz* __restrict__ in, uint32_t G,
                                                  uint32_t nbits, uint32_t nout,
                                                  G1xyzz* __restrict__ out,
                                                  const uint32_t* __restrict__ offsets, uint32_t B,
                                                  uint32_t* __restrict__ entries) {
-  __shared__ G1xyzz sh[4];
+  constexpr uint32_t UPW = QUAD ? 16 : 64;  // units per wave
+  constexpr bool LZ = PLK_BITSUM2_LAZY || QUAD;
+  __shared__ G1xyzz sh[16];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
+  const TailUnit<QUAD> T(tid);
   if (j == 0 && tid == 0) entries[slot] = offsets[(size_t)slot * (B + 1) + B];
   in += (size_t)slot * G * kBitsumOut;
   // lazy additions (one wave per SIMD is all this narrow kernel runs); the stored totals are
-  // finished to [0, 2p) for the host. A lane's first term is taken as is (adding it to
+  // finished to [0, 2p) for the host. A unit's first term is taken as is (adding it to
   // infinity would run the repair path).
   G1R acc = g1r_infinity();
   bool have = false;
-  for (uint32_t g = tid; g < G; g += 256) {
+  for (uint32_t g = T.u; g < G; g += kBitsum2Units(QUAD)) {
     const G1xyzz* e = &in[(size_t)g * kBitsumOut];
     // wide sets: j = nbits sums the plain sums, nbits + 1 the A_g
     uint32_t i0 = kBitsumOut, i1 = kBitsumOut;  // kBitsumOut: none
@@ -1154,24 +1204,30 @@ __global__ void __launch_bounds__(256) k_bitsum2(const G1xyzz* __restrict__ in, 
     for (uint32_t i : {i0, i1}) {
       if (i == kBitsumOut) continue;
       const G1R v = ld_g1r(&e[i]);
-      if (have) acc = g1r_add_t<PLK_BITSUM2_LAZY>(acc, v);
+      if (have) acc = T.template add<LZ>(acc, v);
       else acc = v;
       have = true;
     }
   }
-  // lanes >= G hold infinity: a shuffle tree over each wave's min(G, 64) lanes, then the
-  // wave totals through LDS (768 B instead of a 48 KiB tree)
-  acc = shfl_tree<PLK_BITSUM2_LAZY>(acc, tid & 63, min(G, 64u));
-  const uint32_t nw = min(G, 256u) > 64 ? min(G, 256u) >> 6 : 1;  // waves holding values
-  if ((tid & 63) == 0 && (tid >> 6) < nw) st_g1r(&sh[tid >> 6], acc);
+  // units >= G hold infinity: a shuffle tree over each wave's min(G, UPW) units, then the
+  // wave totals (up to 4 / 8) through LDS
+  uint32_t w0 = 1;
+  while (w0 < min(G, UPW)) w0 <<= 1;
+  acc = T.template tree<LZ>(acc, T.u % UPW, w0);
+  const uint32_t gu = min(G, kBitsum2Units(QUAD)), nw = gu > UPW ? (gu + UPW - 1) / UPW : 1;  // waves holding values
+  if (T.u % UPW == 0 && T.l == 0 && T.u / UPW < nw) st_g1r(&sh[T.u / UPW], acc);
   __syncthreads();
-  if (tid < 2) {  // the (up to) 4 wave totals as a 2-level tree: lanes 0 / 1 add a pair each
-    acc = 2 * tid < nw ? ld_g1r(&sh[2 * tid]) : g1r_infinity();
-    if (2 * tid + 1 < nw) acc = g1r_add_t<PLK_BITSUM2_LAZY>(acc, ld_g1r(&sh[2 * tid + 1]));
-  }
-  if (tid < 64) {  // wave 0 whole: the shuffle reads lane 1
-    const G1R o = shfl_down_g1r(acc, 1);
-    if (tid == 0) st_g1r(&out[(size_t)slot * nout + j], g1r_lazy_finish(nw > 2 ? g1r_add_t<PLK_BITSUM2_LAZY>(acc, o) : acc));
+  if (T.u < UPW) {  // wave 0: unit e < nw/2 adds a pair of wave totals, then a tree
+    const uint32_t e = T.u, np = (nw + 1) / 2;
+    acc = g1r_infinity();
+    if (e < np) {
+      acc = ld_g1r(&sh[2 * e]);
+      if (2 * e + 1 < nw) acc = T.template add<LZ>(acc, ld_g1r(&sh[2 * e + 1]));
+    }
+    uint32_t w = 1;
+    while (w < np) w <<= 1;
+    acc = T.template tree<LZ>(acc, e, w);
+    if (e == 0 && T.l == 0) st_g1r(&out[(size_t)slot * nout + j], g1r_lazy_finish(acc));
   }
 }
 
@@ -1285,6 +1341,28 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
 // d_scalars[k][0 .. lens[k]) (lens[k] <= n_srs) against the SRS prefix, and if
 // check_lens[k] > lens[k] the tail [lens[k], check_lens[k]) must be zero (else that slot
 // reports PLK_E_DEGREE). statuses[k] receives each slot's status.
+// the bit-sum kernels of one batch (k_bitsum2 folded into k_bitsum1 when fold.done is set)
+template <bool QUAD>
+static void bitsum_launch(bool wide, uint32_t G, uint32_t slots, uint32_t NR, uint32_t B,
+                          MsmWorkspace& w, const BitsumFold& fold, uint32_t nbits, uint32_t nout,
+                          G1xyzz* bits_dev, ReadbackHeader* hdr_dev, hipStream_t stream) {
+  constexpr uint32_t S = TailUnit<QUAD>::S;
+  if (wide) {
+    hipLaunchKernelGGL((k_bitsum1<true, QUAD>), dim3(G, slots), dim3(bitsum1_threads(true, QUAD)), 0, stream, NR,
+                       (const G1xyzz*)w.ys.as<G1xyzz>(), (const G1xyzz*)w.zs.as<G1xyzz>(),
+                       w.bits1.as<G1xyzz>(), fold);
+  } else {
+    hipLaunchKernelGGL((k_bitsum1<false, QUAD>), dim3(G, slots), dim3(bitsum1_threads(false, QUAD)), 0, stream, B,
+                       (const G1xyzz*)w.bsum.as<G1xyzz>(), (const G1xyzz*)nullptr,
+                       w.bits1.as<G1xyzz>(), fold);
+  }
+  if (!fold.done) {
+    hipLaunchKernelGGL(k_bitsum2<QUAD>, dim3(nout, slots), dim3(kBitsum2Units(QUAD) * S), 0, stream, w.bits1.as<G1xyzz>(),
+                       G, nbits, nout, bits_dev, (const uint32_t*)w.offsets.as<uint32_t>(), B,
+                       hdr_dev->entries);
+  }
+}
+
 int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const size_t* lens,
                   const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
                   hipStream_t stream) {
@@ -1417,6 +1495,8 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                          w.tasks.as<uint2>(), (uint64_t)w.task_stride);
     }
   }
+  const char* quad_env = getenv("PLK_TAIL_QUAD");  // read per batch: tests flip it
+  const bool quad = PLK_BITSUM_QUAD && (quad_env ? atoi(quad_env) != 0 : w.tail_quad);
   // start / stop events stamped by the dispatch itself (its execution, as rocprofv3 times
   // it), not by the stream: with several lanes on the GPU a stream event would also count
   // the time the kernel waits behind other lanes' kernels
@@ -1449,9 +1529,15 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     const size_t per_bucket = cdiv(total_entries, (size_t)chunk * B * slots) + 1;
     uint32_t lp = 0;
     while (lp < 4 && ((size_t)PLK_LANE_PARTIALS << lp) < per_bucket && (((size_t)B * slots) << lp) < 131072) ++lp;
-    hipLaunchKernelGGL(k_bucket_sum, dim3(cdiv((size_t)B << lp, 256), slots), dim3(256), 0, stream,
-                       w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
-                       w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
+    if (quad) {
+      hipLaunchKernelGGL(k_bucket_sum<true>, dim3(cdiv(((size_t)B << lp) * 4, 256), slots), dim3(256), 0, stream,
+                         w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
+                         w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
+    } else {
+      hipLaunchKernelGGL(k_bucket_sum<false>, dim3(cdiv((size_t)B << lp, 256), slots), dim3(256), 0, stream,
+                         w.task_off.as<uint32_t>(), B, lp, (uint64_t)w.task_stride,
+                         w.partials.as<G1xyzz>(), w.bsum.as<G1xyzz>());
+    }
   }
   BitsumFold fold{};  // k_bitsum2 folded into k_bitsum1 when the slots have few groups
   if (G <= kFoldMaxGroups) {
@@ -1463,20 +1549,8 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     fold.nbits = nbits;
     fold.nout = nout;
   }
-  if (wide) {
-    hipLaunchKernelGGL(k_bitsum1<true>, dim3(G, slots), dim3(192), 0, stream, NR,
-                       (const G1xyzz*)w.ys.as<G1xyzz>(), (const G1xyzz*)w.zs.as<G1xyzz>(),
-                       w.bits1.as<G1xyzz>(), fold);
-  } else {
-    hipLaunchKernelGGL(k_bitsum1<false>, dim3(G, slots), dim3(128), 0, stream, B,
-                       (const G1xyzz*)w.bsum.as<G1xyzz>(), (const G1xyzz*)nullptr,
-                       w.bits1.as<G1xyzz>(), fold);
-  }
-  if (!fold.done) {
-    hipLaunchKernelGGL(k_bitsum2, dim3(nout, slots), dim3(256), 0, stream, w.bits1.as<G1xyzz>(),
-                       G, nbits, nout, bits_dev, (const uint32_t*)w.offsets.as<uint32_t>(), B,
-                       hdr_dev->entries);
-  }
+  if (quad) bitsum_launch<true>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
+  else bitsum_launch<false>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
   PLK_HIP_TRY(hipGetLastError());
 
   // ONE copy of the readback record: flags, entry counts, then the slots' bit sums

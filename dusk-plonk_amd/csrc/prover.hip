@@ -916,6 +916,9 @@ int plk_key_info(const plk_key* key, uint64_t* n, uint64_t* m, plk_g1* commitmen
 }
 
 // ----------------------------------------------------------------------- prover
+#ifndef PLK_LANE_QUAD_MAX_LOG
+#define PLK_LANE_QUAD_MAX_LOG 14
+#endif
 int plk_prover_create(plk_key* key, plk_prover** out) {
   try {
     if (!key || !out) return PLK_E_ARG;
@@ -924,6 +927,11 @@ int plk_prover_create(plk_key* key, plk_prover** out) {
     std::unique_ptr<plk_prover> p(new plk_prover());
     p->key = key;
     p->ws = msm_workspace_new();
+    // a lane shares the chip with other lanes' proofs: its bit sums use the single-lane
+    // additions (fewer issue slots) except for small circuits, whose proofs stay bound by
+    // their reduction chains' latency (msm_common.hpp tail_quad; the default prover of
+    // plk_prove and lone commits keep the quad form)
+    p->ws->tail_quad = key->n <= (1ull << PLK_LANE_QUAD_MAX_LOG);
     PLK_HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->own_stream = true;
     *out = p.release();

@@ -247,3 +247,30 @@ def test_msm_wide_buckets_repeated_points(plk, gpu_ctx, oracle, monkeypatch, tau
     few = np.tile(random_fr(3, seed=80), (n // 3 + 1, 1))[:n].copy()
     for name, s in {"random": sc, "three_values": few, "all_one": np.tile(fr_int(1), (n, 1))}.items():
         assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), name
+
+
+@pytest.mark.parametrize("quad", ["0", "1"])
+@pytest.mark.parametrize("c,logn", [(None, 10), (None, 12), (17, 10), (20, 12)])
+def test_msm_tail_forms(plk, gpu_ctx, oracle, monkeypatch, quad, c, logn):
+    """Both forms of the reduction trees (k_bucket_sum / k_bitsum1 / k_bitsum2, msm.hip):
+    one lane per addition and the quad-cooperative g1r_add_quad, forced with PLK_TAIL_QUAD,
+    on the narrow (default c) and wide (forced c) bucket paths. tau = 1 makes every SRS point
+    G, so equal partial sums meet inside the trees (the quad addition's doubling repair) and
+    opposite ones cancel (its infinity cases); plus random and sparse scalar sets."""
+    monkeypatch.setenv("PLK_TAIL_QUAD", quad)
+    if c:
+        monkeypatch.setenv("PLK_MSM_C", str(c))
+    n = 1 << logn
+    for tau in (fr_int(1)[0], random_fr(1, seed=700 + logn)[0]):
+        pp = plk.PlonkParams.setup(logn, tau, gpu_ctx, n_points=n)
+        pts = pp.points()
+        sc = random_fr(n, seed=701 + logn)
+        cases = {
+            "random": sc,
+            "two_values": np.tile(random_fr(2, seed=702), (n // 2, 1)),
+            "tiny": P.fr_vec_to_np([i % 3 for i in range(n)]),
+            "sparse": np.where((np.arange(n) % 29 == 0)[:, None], sc, 0).astype(np.uint64),
+            "plus_minus": P.fr_vec_to_np([(1 if i % 2 else P.R_MOD - 1) for i in range(n)]),
+        }
+        for name, s in cases.items():
+            assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), (name, quad)
