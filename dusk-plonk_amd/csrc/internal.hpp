@@ -115,6 +115,10 @@ struct plk_srs {
   size_t n = 0;              // number of SRS points
   uint32_t c = 16;           // window bits
   uint32_t windows = 16;     // ceil(256 / c)
+  // the top window's digits (fewer than c - 1 bits when c does not divide 255) are scaled by
+  // 2^top_shift and its table row pre-divided by it (msm_prepare_srs): the same products,
+  // spread over the whole bucket range instead of piled into its low end (msm.hip digit_at)
+  uint32_t top_shift = 0;
   plk::DevBuf points;        // affine, plk::G1Affine (96 B), n entries; inf flags separate
   plk::DevBuf inf;           // uint8 per point
   plk::DevBuf table;         // precomputed 2^(c*w) * P_i, affine, windows * n entries

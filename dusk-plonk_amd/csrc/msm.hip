@@ -48,8 +48,10 @@ namespace {
 constexpr uint32_t kHistThreads = 1024;
 constexpr uint32_t kHistBlocksMax = 256;  // histogram / scatter workgroups per slot
 
-// signed c-bit digit w of canonical scalar s (carry threaded through the caller)
-__device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, uint32_t c, uint32_t& carry) {
+// signed c-bit digit w of canonical scalar s (carry threaded through the caller); the top
+// window's (non-negative, < 2^(c-1 - top_shift)) digit comes scaled by 2^top_shift
+__device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, const MsmCfg& cfg, uint32_t& carry) {
+  const uint32_t c = cfg.c;
   const uint32_t o = w * c;
   uint32_t val = 0;
   if (o < 256) {
@@ -65,7 +67,7 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, uint32_t c, uin
   } else {
     carry = 0;
   }
-  return d;
+  return w + 1 == cfg.W ? d << cfg.top_shift : d;
 }
 
 __device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t& i1) {
@@ -114,7 +116,7 @@ __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cf
       const Fr s = scalar_half(&sc[i], neg);
       uint32_t carry = 0;
       for (uint32_t w = 0; w < cfg.W; ++w) {
-        const int d = digit_at(s, w, cfg.c, carry);
+        const int d = digit_at(s, w, cfg, carry);
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;  // wraps for d == 0
         if (d != 0 && b < nb) atomicAdd(&hist[b], 1u);
       }
@@ -253,7 +255,7 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
       const Fr s = scalar_half(&sc[i], neg);
       uint32_t carry = 0;
       for (uint32_t w = 0; w < cfg.W; ++w) {
-        const int d = digit_at(s, w, cfg.c, carry);
+        const int d = digit_at(s, w, cfg, carry);
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;
         if (d != 0 && b < nb) {
           const uint32_t pos = atomicAdd(&hist[b], 1u);
@@ -450,7 +452,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
     if (tid + k * nt >= len) break;
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(sv[k], w, cfg.c, carry);
+      const int d = digit_at(sv[k], w, cfg, carry);
       if (d != 0) atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
     }
   }
@@ -513,7 +515,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
     if (i >= len) break;
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(sv[k], w, cfg.c, carry);
+      const int d = digit_at(sv[k], w, cfg, carry);
       if (d != 0) {
         const uint32_t pos = atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
         out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != sneg[k]) ? 0x80000000u : 0u);
@@ -609,7 +611,7 @@ __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg c
     const Fr s = scalar_half(&sc[i], neg);
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg.c, carry);
+      const int d = digit_at(s, w, cfg, carry);
       if (d != 0) atomicAdd(&hist[((uint32_t)(d < 0 ? -d : d) - 1u) >> kFineBits], 1u);
     }
   }
@@ -663,7 +665,7 @@ __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCf
     const Fr s = scalar_half(&sc[i], neg);
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg.c, carry);
+      const int d = digit_at(s, w, cfg, carry);
       if (d != 0) {
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
         const uint32_t pos = atomicAdd(&hist[b >> kFineBits], 1u);
@@ -1382,7 +1384,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   }
   int st;
   if ((st = ws_reserve(s, w, max_len ? max_len : 1, (uint32_t)count, stream))) return st;
-  const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1)};
+  const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1), s->top_shift};
   const uint32_t B = cfg.B;
   // wide bucket sets: two-level sort and run-sum reduction; the bit sums then run over the
   // NR = B / 2^rb runs instead of the buckets

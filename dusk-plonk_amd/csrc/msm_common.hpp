@@ -27,6 +27,7 @@ constexpr uint32_t kMaxSlots = 16;  // independent MSMs per batch
 
 struct MsmCfg {
   uint32_t c, W, B;
+  uint32_t top_shift;  // plk_srs::top_shift
 };
 
 // Kernel-argument view of one batch of independent MSMs (slot = blockIdx.y).

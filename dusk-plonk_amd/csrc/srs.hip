@@ -2,7 +2,7 @@
 //
 // setup(k, rng) (zksnarks, un-vendored; tests/*.rs:24) restated with an
 // explicit secret tau: g1[i] = [tau^i] G1. The MSM (msm.hip) additionally needs
-// table[w][i] = 2^(c*w) * g1[i] in affine form; both are produced here with XYZZ
+// table[w][i] = 2^(c*w) * g1[i] in affine form (the top row 2^(c*w - top_shift) g1[i]); both are produced here with XYZZ
 // arithmetic and converted to affine by batch inversion (Montgomery's trick, one Fermat
 // inversion per kBatchAff points).
 #include <hip/hip_runtime.h>
@@ -130,6 +130,16 @@ static uint32_t choose_c(size_t n) {
 int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   s->c = choose_c(s->n);
   s->windows = (255 + s->c - 1) / s->c;  // scalars recoded from [0, (r-1)/2] (< 2^254)
+  // the top window holds bits c (W - 1) .. 253: with the carry its digit is at most
+  // 2^(254 - c (W - 1)); below 2^(c - 1) it is scaled up to span the buckets (plk_srs::top_shift;
+  // c = 20: digits <= 2^14 would pile 2^20 extra entries onto the lowest 2^14 of 2^19 buckets,
+  // doubling the run-sum chains there). PLK_TOP_SPREAD=0: off (experiments)
+  {
+    const int tb = 254 - (int)(s->c * (s->windows - 1));
+    const char* e = getenv("PLK_TOP_SPREAD");
+    const bool on = !e || atoi(e) != 0;
+    s->top_shift = on && tb >= 0 && tb < (int)s->c - 1 ? (uint32_t)((int)s->c - 1 - tb) : 0u;
+  }
   const size_t n = s->n;
   int st;
   if ((st = s->table.alloc((size_t)s->windows * n * sizeof(G1Affine)))) return st;
@@ -144,7 +154,8 @@ int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   uint8_t* tinf = s->table_inf.as<uint8_t>();
   for (uint32_t w = 1; w < s->windows; ++w) {
     hipLaunchKernelGGL(k_double_c, dim3(cdiv(n, 256)), dim3(256), 0, stream, tab + (w - 1) * n,
-                       tinf + (w - 1) * n, (uint64_t)n, s->c, temp.as<G1xyzz>());
+                       tinf + (w - 1) * n, (uint64_t)n,
+                       w + 1 == s->windows ? s->c - s->top_shift : s->c, temp.as<G1xyzz>());
     hipLaunchKernelGGL(k_batch_affine, dim3(cdiv(cdiv(n, kBatchAff), 128)), dim3(128), 0, stream,
                        temp.as<G1xyzz>(), (uint64_t)n, pref.as<Fp>(), tab + w * n, tinf + w * n);
     PLK_HIP_TRY(hipGetLastError());
