@@ -55,9 +55,19 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, const MsmCfg& c
   const uint32_t o = w * c;
   uint32_t val = 0;
   if (o < 256) {
+    // words wd, wd + 1 by a 3-level select tree: indexing s.v with a run-time wd put the
+    // scalar in scratch memory (k_sort_one: 272 B per lane, k_hist / k_scatter: 48)
     const uint32_t wd = o >> 5, sh = o & 31;
-    uint64_t two = s.v[wd];
-    if (wd + 1 < 8) two |= (uint64_t)s.v[wd + 1] << 32;
+    const bool b0 = wd & 1, b1 = wd & 2, b2 = wd & 4;
+    uint64_t p[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // pair (2k + b0, 2k + b0 + 1)
+      const uint32_t lo = b0 ? s.v[2 * k + 1] : s.v[2 * k];
+      const uint32_t hi = b0 ? (k < 3 ? s.v[2 * k + 2] : 0u) : s.v[2 * k + 1];
+      p[k] = ((uint64_t)hi << 32) | lo;
+    }
+    const uint64_t q0 = b1 ? p[1] : p[0], q1 = b1 ? p[3] : p[2];
+    const uint64_t two = b2 ? q1 : q0;
     val = (uint32_t)(two >> sh) & ((1u << c) - 1u);
   }
   int d = (int)(val + carry);
