@@ -423,7 +423,14 @@ __global__ void __launch_bounds__(1024) k_sort_small(uint32_t* __restrict__ bloc
 // sum (exact XYZZ arithmetic, canonical affine result) does not.
 // Measured (profiles/r04_sortone_runsum_shoup_ab.jsonl, one box, interleaved): 2^12 proofs
 // 7.48 / 7.84 against 7.05 / 7.45 M constraints/s with PLK_SORT_ONE=0.
-constexpr uint32_t kSortOneMax = 8192;
+// Round 4, opt-in (PLK_SORT_ONE_BIG, measured no faster): also the 2^14-size proofs' commits
+// (c = 15: 2^14 buckets, ~2^14 scalars per slot), whose multi-workgroup sort is five dispatches
+// per batch (k_hist, k_block_scan, k_scan_buckets, k_scatter, k_make_tasks): KEEP = false
+// re-reads the scalars for the scatter instead of holding them in registers.
+constexpr uint32_t kSortOneMax = 8192;            // KEEP: scalars per slot held in registers
+constexpr uint32_t kSortOneBigMax = 1u << 15;     // !KEEP: scalars per slot
+constexpr uint32_t kSortOneBuckets = 16384;       // LDS counters (64 KiB)
+template <bool KEEP>
 __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, uint64_t n_srs,
                                                    uint32_t chunk, uint32_t* __restrict__ sorted,
                                                    uint64_t sorted_stride,
@@ -431,7 +438,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
                                                    uint32_t* __restrict__ task_off,
                                                    uint2* __restrict__ tasks, uint64_t task_stride,
                                                    uint32_t* __restrict__ flag, uint32_t gen) {
-  __shared__ uint32_t s_count[kSortSmallMax];
+  __shared__ uint32_t s_count[KEEP ? kSortSmallMax : kSortOneBuckets];
   __shared__ uint32_t s_c[1024], s_t[1024], s_f[1024], s_len[kChunkMax], s_cur[kChunkMax];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, nt = 1024, B = cfg.B;  // blockDim.x
   const uint32_t len = batch.len[slot];
@@ -448,22 +455,32 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   __syncthreads();
   // this thread's scalars (i = tid + k nt, at most kSortOneMax / 1024 of them), brought to
   // [0, (r-1)/2] once and kept in registers for both passes
-  constexpr uint32_t kPer = kSortOneMax / 1024;
+  constexpr uint32_t kPer = KEEP ? kSortOneMax / 1024 : 1;
   Fr sv[kPer];
   bool sneg[kPer];
-#pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t i = tid + k * nt;
-    sneg[k] = false;
-    if (i < len) sv[k] = scalar_half(&sc[i], sneg[k]);
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {  // histogram of every digit of the slot
-    if (tid + k * nt >= len) break;
+  auto hist_digits = [&](const Fr& x) {
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(sv[k], w, cfg, carry);
+      const int d = digit_at(x, w, cfg, carry);
       if (d != 0) atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
+    }
+  };
+  if constexpr (KEEP) {
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * nt;
+      sneg[k] = false;
+      if (i < len) sv[k] = scalar_half(&sc[i], sneg[k]);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {  // histogram of every digit of the slot
+      if (tid + k * nt >= len) break;
+      hist_digits(sv[k]);
+    }
+  } else {
+    for (uint32_t i = tid; i < len; i += nt) {
+      bool neg;
+      hist_digits(scalar_half(&sc[i], neg));
     }
   }
   __syncthreads();
@@ -519,17 +536,28 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
     f_run += nfull;
   }
   __syncthreads();
-#pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter, one workgroup)
-    const uint32_t i = tid + k * nt;
-    if (i >= len) break;
+  auto scatter_digits = [&](const Fr& x, bool neg, uint32_t i) {
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(sv[k], w, cfg, carry);
+      const int d = digit_at(x, w, cfg, carry);
       if (d != 0) {
         const uint32_t pos = atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
-        out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != sneg[k]) ? 0x80000000u : 0u);
+        out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
       }
+    }
+  };
+  if constexpr (KEEP) {
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter, one workgroup)
+      const uint32_t i = tid + k * nt;
+      if (i >= len) break;
+      scatter_digits(sv[k], sneg[k], i);
+    }
+  } else {
+    for (uint32_t i = tid; i < len; i += nt) {
+      bool neg;
+      const Fr x = scalar_half(&sc[i], neg);
+      scatter_digits(x, neg, i);
     }
   }
 }
@@ -1063,11 +1091,12 @@ __device__ __forceinline__ uint32_t with_bit(uint32_t k, uint32_t j) {
   return ((k >> j) << (j + 1)) | (1u << j) | (k & ((1u << j) - 1u));
 }
 
-// threads of k_bitsum1: 4 units per row / column sum, 1 or 4 lanes per unit; quads with Z
-// take 2 units per sum (8 members each), so a workgroup stays at 8 waves (2 per SIMD: the quad
-// addition needs ~250 VGPRs)
+// threads of k_bitsum1: 4 units per row / column sum, 1 or 4 lanes per unit. Quads stay at 8
+// waves per workgroup (2 per SIMD: the quad addition needs ~250 VGPRs), so with Z (48 sums) the
+// group takes TWO workgroups (blockIdx.z = role): the 32 row / column sums and their outputs
+// 0..8, and the 16 plain-sum rows and output 9, side by side instead of 8-member chains
 constexpr uint32_t bitsum1_threads(bool z, bool quad) {
-  return quad ? (z ? 384 : 512) : (z ? 192 : 128);
+  return quad ? 512 : (z ? 192 : 128);
 }
 template <bool Z, bool QUAD>
 __global__ void __launch_bounds__(bitsum1_threads(Z, QUAD), PLK_BITSUM_WAVES) k_bitsum1(uint32_t B, const G1xyzz* __restrict__ bsum,
@@ -1085,11 +1114,13 @@ __global__ void __launch_bounds__(bitsum1_threads(Z, QUAD), PLK_BITSUM_WAVES) k_
   // per sum with 2 members each (3-level tree) issued twice the wave-additions (round 3:
   // 8 waves x 4 levels + 4 against 3 waves x 5 levels + 4 per group).
   constexpr uint32_t NS = Z ? 48 : 32;
-  constexpr uint32_t NSU = (QUAD && Z) ? 2 : 4, MEM = 16 / NSU;  // units per sum, members per unit
+  constexpr bool SPLIT = Z && QUAD;  // two workgroups per group (bitsum1_threads)
+  constexpr uint32_t NSU = 4, MEM = 16 / NSU;  // units per sum, members per unit
   constexpr uint32_t NU = bitsum1_threads(Z, QUAD) / TailUnit<QUAD>::S;  // units
   constexpr bool LZ = PLK_BITSUM_LAZY;
   __shared__ G1xyzz sh[NS];
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  const uint32_t role = SPLIT ? blockIdx.z : 0;
   const TailUnit<QUAD> T(tid);
   out += ((size_t)slot * gridDim.x + g) * kBitsumOut;
   auto value = [&](uint32_t x) -> G1R {  // x < 256: bsum, else zin; past B: infinity
@@ -1100,23 +1131,26 @@ __global__ void __launch_bounds__(bitsum1_threads(Z, QUAD), PLK_BITSUM_WAVES) k_
   {  // sum q < 16: row a = q (members 16q + c); 16 <= q < 32: column c = q - 16 (members
      // c + 16a); q >= 32 (Z): row q - 32 of the plain-sum values. Unit e < NSU of the sum's
      // NSU takes members MEM e .. MEM e + MEM - 1 of its row / column.
-    const uint32_t q = T.u / NSU, e = T.u % NSU;
+    const uint32_t q = T.u / NSU + (role ? 32 : 0), e = T.u % NSU;
     auto member = [&](uint32_t i) {  // i-th member of sum q, i < 16
       return q < 16 ? 16 * q + i : q < 32 ? (q - 16) + 16 * i : 256 + 16 * (q - 32) + i;
     };
-    G1R acc = value(member(MEM * e));
+    if (q < NS && (!SPLIT || role || q < 32)) {  // uniform per sum (its NSU units)
+      G1R acc = value(member(MEM * e));
 #pragma unroll 1
-    for (uint32_t i = 1; i < MEM; ++i) acc = T.template add<LZ>(acc, value(member(MEM * e + i)));
-    acc = T.template tree<LZ>(acc, e, NSU);
-    if (e == 0 && T.l == 0) st_g1r(&sh[q], acc);
+      for (uint32_t i = 1; i < MEM; ++i) acc = T.template add<LZ>(acc, value(member(MEM * e + i)));
+      acc = T.template tree<LZ>(acc, e, NSU);
+      if (e == 0 && T.l == 0) st_g1r(&sh[q], acc);
+    }
   }
   __syncthreads();
   // units 0..31 = T_0..T_7, 4 units each (2 terms per unit); units 32..39 = A_g, 8 units
   // (rows 2e, 2e + 1); with Z units 40..47 = the plain sum (its rows 2e, 2e + 1); then trees
   // (unit groups never straddle a wave: 4 or 8 units of 1 or 4 lanes, aligned)
   if (T.u < 64) {
-    const uint32_t t = T.u;
-    const bool on = t < (Z ? 48u : 40u);
+    // (SPLIT: role 0 the units 0..39, role 1 the plain sum as units 40..47)
+    const uint32_t t = role ? 40 + T.u : T.u;
+    const bool on = role ? T.u < 8 : t < (Z && !SPLIT ? 48u : 40u);
     const uint32_t s = t < 32 ? t >> 2 : t < 40 ? 8 : 9, e = t < 32 ? t & 3 : (t - 32) & 7;
     const uint32_t w = t < 32 ? 4 : 8;
     uint32_t i0 = 0, i1 = 0;
@@ -1145,7 +1179,7 @@ __global__ void __launch_bounds__(bitsum1_threads(Z, QUAD), PLK_BITSUM_WAVES) k_
   __shared__ uint32_t s_last;
   __threadfence();
   __syncthreads();
-  if (tid == 0) s_last = atomicAdd(&fold.done[slot], 1u) == gridDim.x - 1 ? 1u : 0u;
+  if (tid == 0) s_last = atomicAdd(&fold.done[slot], 1u) == gridDim.x * gridDim.z - 1 ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
   __threadfence();
@@ -1360,7 +1394,7 @@ static void bitsum_launch(bool wide, uint32_t G, uint32_t slots, uint32_t NR, ui
                           G1xyzz* bits_dev, ReadbackHeader* hdr_dev, hipStream_t stream) {
   constexpr uint32_t S = TailUnit<QUAD>::S;
   if (wide) {
-    hipLaunchKernelGGL((k_bitsum1<true, QUAD>), dim3(G, slots), dim3(bitsum1_threads(true, QUAD)), 0, stream, NR,
+    hipLaunchKernelGGL((k_bitsum1<true, QUAD>), dim3(G, slots, QUAD ? 2 : 1), dim3(bitsum1_threads(true, QUAD)), 0, stream, NR,
                        (const G1xyzz*)w.ys.as<G1xyzz>(), (const G1xyzz*)w.zs.as<G1xyzz>(),
                        w.bits1.as<G1xyzz>(), fold);
   } else {
@@ -1435,7 +1469,14 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
 #ifndef PLK_SORT_ONE
 #define PLK_SORT_ONE 1
 #endif
-  const bool sort_one = PLK_SORT_ONE && small_batch;
+#ifndef PLK_SORT_ONE_BIG  // opt-in: 2^14 proofs 14.8-15.3 against 15.1-15.2 M constraints/s
+#define PLK_SORT_ONE_BIG 0  // without it (profiles/r04_sort_one_big_ab.jsonl): the dispatches saved
+#endif                      // do not pay for one workgroup sorting ~280 K digits per commit
+  // KEEP form for small batches; the re-reading form up to 2^14 buckets / 2^15 scalars for
+  // batches of several commits (one workgroup per slot: a lone commit keeps the
+  // multi-workgroup sort, whose latency is lower)
+  const bool sort_one_big = !wide && count > 1 && B <= kSortOneBuckets && max_len <= kSortOneBigMax;
+  const bool sort_one = PLK_SORT_ONE && (small_batch || (PLK_SORT_ONE_BIG && sort_one_big));
   if (max_tail && !sort_one) {
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
                        batch, hdr_dev->flag, gen);
@@ -1468,10 +1509,17 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        (const uint32_t*)w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>(),
                        w.task_off.as<uint32_t>(), w.tasks.as<uint2>(), (uint64_t)w.task_stride);
   } else if (sort_one) {
-    hipLaunchKernelGGL(k_sort_one, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
-                       (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
-                       w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
-                       (uint64_t)w.task_stride, hdr_dev->flag, gen);
+    if (small_batch) {
+      hipLaunchKernelGGL(k_sort_one<true>, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
+                         (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
+                         w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
+                         (uint64_t)w.task_stride, hdr_dev->flag, gen);
+    } else {
+      hipLaunchKernelGGL(k_sort_one<false>, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
+                         (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
+                         w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
+                         (uint64_t)w.task_stride, hdr_dev->flag, gen);
+    }
   } else {
     const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
     if (max_len) {

@@ -122,17 +122,17 @@ __global__ void k_perm_numden(const Fr* __restrict__ wires, const Fr* __restrict
   if (i >= n) return;
   const RFr be = rx_unpack(beta_rx), g = rx_unpack(gamma);
   const RFr bx = rx_mul(be, ldr(&elements[i]));
-  const RFr bxk[4] = {bx, rx_mul(rx_unpack(k1_rx), bx), rx_mul(rx_unpack(k2_rx), bx),
-                      rx_mul(rx_unpack(k3_rx), bx)};
-  RFr nu, de;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const RFr w = ldr(&wires[c * n + i]);
-    const RFr tn = add3_u(w, g, bxk[c]);
-    const RFr td = add3_u(w, g, rx_mul(be, ldr(&sigmas[c * n + i])));
-    nu = c == 0 ? rx_norm(tn) : rx_mul(nu, tn);
-    de = c == 0 ? rx_norm(td) : rx_mul(de, td);
-  }
+  // the four wire factors written out (a loop over an array of the bX K_c values kept the
+  // array in scratch memory)
+  auto tn = [&](int c, const RFr& bxk) { return add3_u(ldr(&wires[c * n + i]), g, bxk); };
+  auto td = [&](int c) { return add3_u(ldr(&wires[c * n + i]), g, rx_mul(be, ldr(&sigmas[c * n + i]))); };
+  RFr nu = rx_norm(tn(0, bx)), de = rx_norm(td(0));
+  nu = rx_mul(nu, tn(1, rx_mul(rx_unpack(k1_rx), bx)));
+  de = rx_mul(de, td(1));
+  nu = rx_mul(nu, tn(2, rx_mul(rx_unpack(k2_rx), bx)));
+  de = rx_mul(de, td(2));
+  nu = rx_mul(nu, tn(3, rx_mul(rx_unpack(k3_rx), bx)));
+  de = rx_mul(de, td(3));
   const RFr f = rx_unpack(fix);
   stf(&num[i], rx_pack_canonical(rx_mul(nu, f)));
   stf(&den[i], rx_pack_canonical(rx_mul(de, f)));
