@@ -125,7 +125,10 @@ struct RxPlan {
         const long double bj = (long double)(1ull << (j == L - 1 ? TOP_BITS : B));
         sum += NPROD * ai * bj + (long double)(1ull << B) * (long double)(K.p[j] + 1);
       }
-      split[k] = sum >= 18446744073709551616.0L;  // 2^64 (exact worst case)
+      // 2^64. The sum is exact in long double on the host and rounded in the device pass
+      // (long double is double there): the closest unsplit column sits at 0.993 x 2^64, far
+      // outside double's 2^-52 relative error, so both passes give the same plan
+      split[k] = sum >= 18446744073709551616.0L;
       carry = sum / (long double)(1ull << B) + 4;
     }
   }
