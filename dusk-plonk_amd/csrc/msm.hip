@@ -1388,11 +1388,10 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
 // check_lens[k] > lens[k] the tail [lens[k], check_lens[k]) must be zero (else that slot
 // reports PLK_E_DEGREE). statuses[k] receives each slot's status.
 // the bit-sum kernels of one batch (k_bitsum2 folded into k_bitsum1 when fold.done is set)
-template <bool QUAD>
+template <bool QUAD, bool QUAD2>
 static void bitsum_launch(bool wide, uint32_t G, uint32_t slots, uint32_t NR, uint32_t B,
                           MsmWorkspace& w, const BitsumFold& fold, uint32_t nbits, uint32_t nout,
                           G1xyzz* bits_dev, ReadbackHeader* hdr_dev, hipStream_t stream) {
-  constexpr uint32_t S = TailUnit<QUAD>::S;
   if (wide) {
     hipLaunchKernelGGL((k_bitsum1<true, QUAD>), dim3(G, slots, QUAD ? 2 : 1), dim3(bitsum1_threads(true, QUAD)), 0, stream, NR,
                        (const G1xyzz*)w.ys.as<G1xyzz>(), (const G1xyzz*)w.zs.as<G1xyzz>(),
@@ -1403,7 +1402,7 @@ static void bitsum_launch(bool wide, uint32_t G, uint32_t slots, uint32_t NR, ui
                        w.bits1.as<G1xyzz>(), fold);
   }
   if (!fold.done) {
-    hipLaunchKernelGGL(k_bitsum2<QUAD>, dim3(nout, slots), dim3(kBitsum2Units(QUAD) * S), 0, stream, w.bits1.as<G1xyzz>(),
+    hipLaunchKernelGGL(k_bitsum2<QUAD2>, dim3(nout, slots), dim3(kBitsum2Units(QUAD2) * TailUnit<QUAD2>::S), 0, stream, w.bits1.as<G1xyzz>(),
                        G, nbits, nout, bits_dev, (const uint32_t*)w.offsets.as<uint32_t>(), B,
                        hdr_dev->entries);
   }
@@ -1556,7 +1555,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     }
   }
   const char* quad_env = getenv("PLK_TAIL_QUAD");  // read per batch: tests flip it
-  const bool quad = PLK_BITSUM_QUAD && (quad_env ? atoi(quad_env) != 0 : w.tail_quad);
+  // 0: single-lane trees, 1: quad trees, 2: quad k_bitsum2 only (its few workgroups are
+  // latency-bound at any load)
+  const int tail = !PLK_BITSUM_QUAD ? 0 : quad_env ? atoi(quad_env) : w.tail_quad;
+  const bool quad = tail == 1;
   // start / stop events stamped by the dispatch itself (its execution, as rocprofv3 times
   // it), not by the stream: with several lanes on the GPU a stream event would also count
   // the time the kernel waits behind other lanes' kernels
@@ -1609,8 +1611,9 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     fold.nbits = nbits;
     fold.nout = nout;
   }
-  if (quad) bitsum_launch<true>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
-  else bitsum_launch<false>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
+  if (quad) bitsum_launch<true, true>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
+  else if (tail == 2) bitsum_launch<false, true>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
+  else bitsum_launch<false, false>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
   PLK_HIP_TRY(hipGetLastError());
 
   // ONE copy of the readback record: flags, entry counts, then the slots' bit sums

@@ -109,10 +109,11 @@ struct MsmWorkspace {
   // above depends on c and the window count
   uint32_t cap_c = 0, cap_windows = 0;
   uint32_t cap_chunk_min = kChunkMin;  // the task-length floor the buffers were sized for
-  // the bit-sum trees' additions: quad-cooperative (g1r_add_quad, lower latency, the lone
-  // call's choice) or one lane each (fewer issue slots per addition, for prover lanes that
-  // share the chip with other proofs); PLK_TAIL_QUAD=0/1 overrides (experiments)
-  bool tail_quad = true;
+  // the bit-sum trees' additions: 1 quad-cooperative (g1r_add_quad, lower latency, the lone
+  // call's choice), 0 one lane each (fewer issue slots per addition, for prover lanes that
+  // share the chip with other proofs), 2 quads in k_bitsum2 only; PLK_TAIL_QUAD overrides
+  // (experiments)
+  int tail_quad = 1;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   MsmStats stats;
   ~MsmWorkspace() {

@@ -931,7 +931,9 @@ int plk_prover_create(plk_key* key, plk_prover** out) {
     // additions (fewer issue slots) except for small circuits, whose proofs stay bound by
     // their reduction chains' latency (msm_common.hpp tail_quad; the default prover of
     // plk_prove and lone commits keep the quad form)
-    p->ws->tail_quad = key->n <= (1ull << PLK_LANE_QUAD_MAX_LOG);
+    // 2^19 and up: quads in k_bitsum2 only (2^20 proofs +0.6 %, three of three interleaved
+    // runs; 2^16 -3 %: profiles/r04_tail_mode2_ab.jsonl)
+    p->ws->tail_quad = key->n <= (1ull << PLK_LANE_QUAD_MAX_LOG) ? 1 : key->n >= (1ull << 19) ? 2 : 0;
     PLK_HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->own_stream = true;
     *out = p.release();

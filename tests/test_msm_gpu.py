@@ -249,11 +249,12 @@ def test_msm_wide_buckets_repeated_points(plk, gpu_ctx, oracle, monkeypatch, tau
         assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), name
 
 
-@pytest.mark.parametrize("quad", ["0", "1"])
+@pytest.mark.parametrize("quad", ["0", "1", "2"])
 @pytest.mark.parametrize("c,logn", [(None, 10), (None, 12), (17, 10), (20, 12)])
 def test_msm_tail_forms(plk, gpu_ctx, oracle, monkeypatch, quad, c, logn):
-    """Both forms of the reduction trees (k_bucket_sum / k_bitsum1 / k_bitsum2, msm.hip):
-    one lane per addition and the quad-cooperative g1r_add_quad, forced with PLK_TAIL_QUAD,
+    """The forms of the reduction trees (k_bucket_sum / k_bitsum1 / k_bitsum2, msm.hip):
+    one lane per addition, the quad-cooperative g1r_add_quad, and quads in k_bitsum2 only
+    (PLK_TAIL_QUAD = 0 / 1 / 2),
     on the narrow (default c) and wide (forced c) bucket paths. tau = 1 makes every SRS point
     G, so equal partial sums meet inside the trees (the quad addition's doubling repair) and
     opposite ones cancel (its infinity cases); plus random and sparse scalar sets."""
