@@ -531,9 +531,11 @@ __global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restric
 // Ruffini for small polynomials (len <= kRuffiniSingleMax) in ONE dispatch instead of five
 // (pk_ruffini: scale powers, 3-phase scan, scale powers): q_k = z^-(k+1) sum_(i>k) c_i z^i.
 // A workgroup of 1 024 threads; thread t owns j in [tE, tE + E) (E = ceil(len / 1024) <= 16).
-// Pass 1 (upward) forms y_j = c_j z^j and the thread's sum; an exclusive suffix scan of the
-// sums over the threads (LDS) gives each thread the sum of y above its range; pass 2 walks
-// its range downward with that running sum. Start powers z^(tE) and z^-(tE+1) come from
+// Pass 1 (upward) forms y_j = c_j z^j and the thread's sum, parking y_j in q[j]; an exclusive
+// suffix scan of the sums over the threads (LDS) gives each thread the sum of y above its
+// range; pass 2 walks its range downward with that running sum (2 products per element there
+// instead of 4: y_j is read back, not recomputed; 2^12 proofs within noise of the round-3 form,
+// profiles/r04_ruffini_park_ab.jsonl). Start powers z^(tE) and z^-(tE+1) come from
 // product scans of z^E / z^-E in LDS. All powers R'-domain (the host converts), products in
 // the R domain, outputs canonical: the same field values as the five-dispatch form.
 constexpr uint32_t kRuffiniThreads = 1024, kRuffiniSingleMax = 16 * kRuffiniThreads;
@@ -560,9 +562,14 @@ __global__ void __launch_bounds__(kRuffiniThreads) k_ruffini_single(const Fr* __
   const RFr zr = rx_unpack(z), zir = rx_unpack(zi);
   RFr pw = rx_unpack(T[tid]);   // z^j0
   RFr pwi = rx_unpack(U[tid]);  // z^-(j0 + 1)
-  Fr loc = fe_zero<FrCfg>();
+  Fr loc = fe_zero<FrCfg>(), ylast = fe_zero<FrCfg>();
   for (uint64_t j = j0; j < j1; ++j) {  // pass 1: this thread's sum of y_j
-    loc = fe_add(loc, rx_pack_canonical(rx_mul(ldr(&c[j]), pw)));
+    const Fr y = rx_pack_canonical(rx_mul(ldr(&c[j]), pw));
+    loc = fe_add(loc, y);
+    // y_j parked in q[j] for pass 2 (q[j] is this thread's and is rewritten there; q holds
+    // len - 1 entries, so the top y stays in a register)
+    if (j + 1 < len) stf(&q[j], y);
+    else ylast = y;
     pw = rx_mul(pw, zr);
     pwi = rx_mul(pwi, zir);
   }
@@ -576,12 +583,12 @@ __global__ void __launch_bounds__(kRuffiniThreads) k_ruffini_single(const Fr* __
     __syncthreads();
   }
   Fr run = fe_sub(T[tid], loc);  // sum of y_i over i >= j1
-  // pass 2, downward from j1 - 1: pw = z^j1 -> z^k, pwi = z^-(j1 + 1) -> z^-(k + 1)
+  // pass 2, downward from j1 - 1: pwi = z^-(j1 + 1) -> z^-(k + 1); y_k back from q[k]
   for (uint64_t k = j1; k-- > j0;) {
-    pw = rx_mul(pw, zir);
     pwi = rx_mul(pwi, zr);
-    const Fr yk = rx_pack_canonical(rx_mul(ldr(&c[k]), pw));  // read before q[k] (q may be c)
-    if (k + 1 < len) stf(&q[k], rx_pack_canonical(rx_mul(rx_unpack(run), pwi)));
+    const bool in_q = k + 1 < len;
+    const Fr yk = in_q ? ldf(&q[k]) : ylast;  // read before q[k] is rewritten
+    if (in_q) stf(&q[k], rx_pack_canonical(rx_mul(rx_unpack(run), pwi)));
     run = fe_add(run, yk);
   }
 }
