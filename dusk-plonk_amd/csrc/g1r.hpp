@@ -310,7 +310,8 @@ __device__ __forceinline__ G1R g1r_add_lazy(const G1R& p, const G1R& q) {
 // uniform per quad). Measured (profiles/r04_tail_quad_ab.jsonl): lone MSMs 2^16 0.82 -> 0.68 ms,
 // 2^20 3.30 -> 3.01-3.10 ms; 2^12 proofs +8-15 %; proofs at 2^16 / 2^20, where other lanes'
 // kernels fill the chip, ~1 % slower (more issue slots per addition): prover lanes above
-// 2^14 keep the single-lane trees (msm_common.hpp tail_quad).
+// 2^13 keep single-lane trees, with quads in k_bitsum2 alone at 2^14 and from 2^19
+// (msm_common.hpp tail_quad, prover.hip plk_prover_create).
 template <int K>
 __device__ __forceinline__ RFp quad_bcast(const RFp& v) {
   RFp r;
