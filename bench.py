@@ -115,7 +115,16 @@ def parse():
     ap.add_argument("--shard-msm", action="store_true",
                     help="BASELINE configs[4]: all ranks prove the same proofs, every commit "
                          "split over the ranks by SRS slice (RCCL all-gather of partial points "
-                         "+ host fold); NTT / elementwise rounds replicated")
+                         "+ host fold); NTT / elementwise rounds replicated. With --mode msm: "
+                         "ONE MSM per step split over the ranks (--msm-split)")
+    ap.add_argument("--msm-split", choices=["buckets", "points"], default="buckets",
+                    help="--mode msm --shard-msm: by bucket range (each rank sorts, accumulates "
+                         "and reduces 1/G of the buckets; plk_commit_batch_dev_part) or by SRS "
+                         "slice (each rank the whole Pippenger over 1/G of the points)")
+    ap.add_argument("--bucket-parts", type=int, default=1,
+                    help="--mode msm on ONE GPU: run the MSM as P bucket-range parts one after "
+                         "the other (what each of P GPUs would run under --shard-msm), timing "
+                         "each part; the line reports the per-part times and checks the fold")
     return ap.parse_args()
 
 
@@ -800,7 +809,8 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
     (tests/oracle_lib.py), whose timing on the same input is the cpu_baseline."""
     s = torch.cuda.current_stream().cuda_stream
     ctx = plk.Context.default(device.index or 0)
-    x = rand_fr_dev(torch, n, 4242 + rank, device)
+    # a split MSM (--shard-msm): every rank holds the same scalars; replicas: their own
+    x = rand_fr_dev(torch, n, 4242 if args.shard_msm else 4242 + rank, device)
     ev = []
     if args.mode == "ntt":
         fft = plk.Fft(k, ctx)
@@ -821,13 +831,54 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
     else:
         tau = np.asarray(np.random.default_rng(0x5EED).integers(1, 2**62, 4), dtype=np.uint64)
         tau[3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
-        pp = plk.PlonkParams.setup(k, tau, ctx)
         coms = []
+        part_s = []  # per step: [seconds of each bucket-range part] (--bucket-parts / --shard-msm)
+        if args.shard_msm:  # one MSM per step split over the ranks (strong scaling)
+            from dusk_plonk_amd.parallel import ShardedPlonkParams
+            spp = ShardedPlonkParams(k, tau, ctx=ctx, mode=args.msm_split)
+            pp = spp.local
+            comm_dev = device if dist.get_backend() == "nccl" else None
 
-        def step(timed):
-            coms.append(pp.commit_dev(x.data_ptr(), n, s))  # returns the affine point
-            if timed:
-                ev.append(pp.last_msm_stats())
+            def step(timed):
+                t0 = time.perf_counter()
+                part = pp.commit_batch_dev([(x.data_ptr(), n)], s, raise_on_error=False,
+                                           **({"part": rank, "parts": world}
+                                              if spp.mode == "buckets" else {}))
+                t1 = time.perf_counter()
+                from dusk_plonk_amd.parallel import gather_fold
+                w = np.zeros((1, 13), dtype=np.uint64)
+                w[0] = part[0].words
+                coms.append(gather_fold(w, [0], None, comm_dev)[0])
+                if timed:
+                    ev.append(pp.last_msm_stats())
+                    part_s.append([t1 - t0])
+        elif args.bucket_parts > 1:  # the G parts of a bucket-split MSM, one after the other
+            from dusk_plonk_amd.parallel import bucket_parts_ok
+            P = args.bucket_parts
+            pp = plk.PlonkParams.setup(k, tau, ctx)
+            if not bucket_parts_ok(pp.n, P):
+                raise SystemExit(f"bench.py: --bucket-parts {P} not valid for 2^{k} points")
+
+            def step(timed):
+                ts, pts, st = [], [], (0.0, 0, 0)
+                for q in range(P):
+                    t0 = time.perf_counter()
+                    c = pp.commit_batch_dev([(x.data_ptr(), n)], s, part=q, parts=P)[0]
+                    ts.append(time.perf_counter() - t0)
+                    pts.append(c.words)
+                    ms_q, adds_q, cb = pp.last_msm_stats()
+                    st = (st[0] + ms_q, st[1] + adds_q, cb)
+                coms.append(plk.g1_sum(np.stack(pts)))
+                if timed:
+                    ev.append(st)
+                    part_s.append(ts)
+        else:
+            pp = plk.PlonkParams.setup(k, tau, ctx)
+
+            def step(timed):
+                coms.append(pp.commit_dev(x.data_ptr(), n, s))  # returns the affine point
+                if timed:
+                    ev.append(pp.last_msm_stats())
         units = n
     for _ in range(args.warmup):
         step(False)
@@ -882,16 +933,39 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
                      "note": "integer-VALU-bound (no MFMA); HBM is the secondary roofline"})
         metric = f"standalone G1 MSM points/s at n=2^{k} (BASELINE configs[2])"
         workload = f"KZG10 commit: one 2^{k}-point G1 MSM, random Fr scalars, SRS bases"
+        if part_s:
+            per = np.asarray(part_s) * 1e3  # [steps, parts] ms
+            roof["bucket_parts"] = {
+                "parts": per.shape[1] if not args.shard_msm else world,
+                "part_ms_mean": [float(v) for v in per.mean(axis=0)],
+                "part_ms_max": float(per.mean(axis=0).max()),
+                "note": ("each part = plk_commit_batch_dev_part on this GPU: reads every scalar "
+                         "and the whole window table, sorts / accumulates / reduces only its "
+                         "bucket range; host-timed (launch to readback). Under --shard-msm the "
+                         "rank's own part; with --bucket-parts the parts ran one after the other "
+                         "on one GPU, each as one of G GPUs would run it")}
+            if args.shard_msm:
+                workload += (f"; split over {world} GPU(s) by "
+                             + ("bucket range" if spp.mode == "buckets" else "SRS slice")
+                             + f" ({transport(dist)} all-gather of one point per rank + host fold)")
+            else:
+                workload += (f"; run as {per.shape[1]} bucket-range parts one after the other on "
+                             "one GPU (the per-GPU work of a split over that many GPUs) + host fold")
     if "frac" not in roof:
         roof["frac"] = roof["achieved"] / roof["peak"]
     result = {
-        "metric": metric, "value": units * steps * world / elapsed, "unit": "points/s",
+        "metric": metric,
+        "value": units * steps * (1 if (args.shard_msm and args.mode == "msm") else world) / elapsed,
+        "unit": "points/s",
         "n_gpus": world, "steps": steps, "warmup": args.warmup,
-        "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True,
+        "scaling": "strong" if (args.shard_msm and args.mode == "msm") else "weak",
         "vs_baseline": None, "dtype": "u32-limb Montgomery Fr/Fp (integer)",
         "data": "synthetic (uniform Fr)",
         "config": {"workload": workload, "n": n, "log_n": k,
-                   "parallelism": f"replicas x{world}"},
+                   "parallelism": (f"msm-split x{world} ({args.msm_split})"
+                                   if (args.shard_msm and args.mode == "msm") else
+                                   f"replicas x{world}")},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -414,6 +414,12 @@ int plk_commit_dev(plk_srs* s, const plk_fr* d_coeffs, size_t len, plk_g1* out, 
 
 int plk_commit_batch_dev(plk_srs* s, const plk_fr* const* d_coeffs, const size_t* lens,
                          size_t count, plk_g1* outs, int* statuses, void* stream) {
+  return plk_commit_batch_dev_part(s, d_coeffs, lens, count, 0, 1, outs, statuses, stream);
+}
+
+int plk_commit_batch_dev_part(plk_srs* s, const plk_fr* const* d_coeffs, const size_t* lens,
+                              size_t count, uint32_t part, uint32_t parts, plk_g1* outs,
+                              int* statuses, void* stream) {
   PLK_API_BEGIN
   if (!s || !outs || (count && (!d_coeffs || !lens))) return PLK_E_ARG;
   for (size_t k = 0; k < count; ++k)
@@ -430,7 +436,8 @@ int plk_commit_batch_dev(plk_srs* s, const plk_fr* const* d_coeffs, const size_t
       chk[k] = lens[base + k];
       use[k] = chk[k] < s->n ? chk[k] : s->n;
     }
-    const int r = msm_run_batch(s, *s->ws, ptrs, use, chk, m, outs + base, statuses ? statuses + base : nullptr, st);
+    const int r = msm_run_batch(s, *s->ws, ptrs, use, chk, m, outs + base,
+                                statuses ? statuses + base : nullptr, st, part, parts);
     if (r != PLK_OK && r != PLK_E_DEGREE) return r;
     if (r != PLK_OK && overall == PLK_OK) overall = r;
   }

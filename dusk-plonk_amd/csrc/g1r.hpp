@@ -136,7 +136,35 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
 #define PLK_MADD_GROUPED 1
 #endif
 __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, const RFp& y2) {
-#if PLK_MADD_GROUPED
+#if PLK_MADD_GROUPED == 2
+  // round-4 experiment, rebuilt in round 5 to find the libplk-g2 abort: (U2, S2), (PP, R^2),
+  // (PPP, Q, ZZ3), (Y3, ZZZ3)
+  RFp U2, S2, PP, RR, PPP, Q;
+  rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
+  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
+  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
+  rx_sqr2(P, R, PP, RR);
+  G1R r;
+  rx_mul3(P, PP, p.X, PP, p.ZZ, PP, PPP, Q, r.ZZ);
+  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
+  rx_mul_add_mul(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP,
+                 p.ZZZ, PPP, r.Y, r.ZZZ);
+  return r;
+#elif PLK_MADD_GROUPED == 3
+  // pairs chosen for the smallest live set (3 waves per SIMD): (U2, S2), (PP, R^2),
+  // (PPP, ZZ3), (Q, ZZZ3), then Y3 alone
+  RFp U2, S2, PP, RR, PPP, Q;
+  rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
+  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
+  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
+  rx_sqr2(P, R, PP, RR);
+  G1R r;
+  rx_mul2(P, PP, p.ZZ, PP, PPP, r.ZZ);
+  rx_mul2(p.X, PP, p.ZZZ, PPP, Q, r.ZZZ);
+  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
+  r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP);
+  return r;
+#elif PLK_MADD_GROUPED
   // the same nine reductions as independent groups whose chains interleave (ffr.hpp
   // rx_prod_group): (U2, S2), (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3). (PPP, Q, ZZ3) then
   // (Y3, ZZZ3) compiled to 402 instead of 536 s_nop but issued at the same rate (6.58-6.61e9

@@ -233,9 +233,13 @@ int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g
             hipStream_t stream);
 // The SRS (window table) is only read: any number of threads may run batches on one SRS
 // concurrently, each with its own workspace `w` and stream.
+// part / parts (parts a power of two, 1 = the whole MSM): only the buckets of the part's
+// range [part, part + 1) * 2^(c-1) / parts (wide bucket sets, 2^(c-1) / parts >= 2^14); the
+// parts' outputs sum to the whole MSM's (one large MSM split over GPUs by bucket
+// range, each GPU's reduction over its own buckets only).
 int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const size_t* lens,
                   const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
-                  hipStream_t stream);
+                  hipStream_t stream, uint32_t part = 0, uint32_t parts = 1);
 MsmWorkspace* msm_workspace_new();
 void msm_workspace_delete(MsmWorkspace* w);
 const MsmStats& msm_workspace_stats(const MsmWorkspace& w);

@@ -650,7 +650,8 @@ __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg c
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
       const int d = digit_at(s, w, cfg, carry);
-      if (d != 0) atomicAdd(&hist[((uint32_t)(d < 0 ? -d : d) - 1u) >> kFineBits], 1u);
+      const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
+      if (b < cfg.B) atomicAdd(&hist[b >> kFineBits], 1u);
     }
   }
   __syncthreads();
@@ -704,8 +705,8 @@ __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCf
     uint32_t carry = 0;
     for (uint32_t w = 0; w < cfg.W; ++w) {
       const int d = digit_at(s, w, cfg, carry);
-      if (d != 0) {
-        const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
+      const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
+      if (b < cfg.B) {
         const uint32_t pos = atomicAdd(&hist[b >> kFineBits], 1u);
         out[pos] = make_uint2((uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u), b);
       }
@@ -834,67 +835,6 @@ __global__ void __launch_bounds__(kFine) k_make_tasks_wide(uint32_t B, uint32_t 
   if (tail)
     tasks[s_base[tail] + rank] =
         make_uint2(start + nfull * chunk, (t0 + nfull) | ((tail - 1) << kTaskShift));
-}
-
-#ifndef PLK_ACC_WAVES
-#define PLK_ACC_WAVES 1  // min waves per SIMD requested from the register allocator
-#endif
-template <bool HAS_INF>
-__global__ void __launch_bounds__(256, PLK_ACC_WAVES) k_accumulate(const uint2* __restrict__ tasks,
-                                                    const uint32_t* __restrict__ task_off,
-                                                    uint32_t B, uint64_t task_stride,
-                                                    const uint32_t* __restrict__ sorted,
-                                                    uint64_t sorted_stride,
-                                                    const G1Affine* __restrict__ table,
-                                                    const uint8_t* __restrict__ table_inf,
-                                                    G1xyzz* __restrict__ partials) {
-  const uint32_t slot = blockIdx.y;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= task_off[(size_t)slot * (B + 1) + B]) return;
-  const uint2 tk = tasks[(size_t)slot * task_stride + t];
-  const uint2 task = make_uint2(tk.x, (tk.y >> kTaskShift) + 1);  // first entry, length (>= 1)
-  const uint32_t pidx = tk.y & ((1u << kTaskShift) - 1);
-  sorted += (size_t)slot * sorted_stride;
-  // software-pipelined: the next entry's index and point are loaded before the current
-  // mixed add, so the two dependent loads overlap the ~5k-instruction madd (+8%,
-  // tools/ubench_acc.hip). The first entry initialises the accumulator; exceptional
-  // additions (accumulator at infinity, equal x) show up as ZZ3 == 0 after the
-  // straight-line formula and are finished with the point reloaded (g1r.hpp).
-  const uint32_t end = task.x + task.y;
-  G1R acc = g1r_infinity();
-  {
-    const uint32_t c0 = sorted[task.x];
-    if (!HAS_INF || !table_inf[c0 & 0x7fffffffu]) {
-      ld_g1r_aff(&table[c0 & 0x7fffffffu], acc.X, acc.Y);
-      if (c0 & 0x80000000u) acc.Y = rx_neg(acc.Y);
-      acc.ZZ = rx_one<FpCfg>();
-      acc.ZZZ = rx_one<FpCfg>();
-    }
-  }
-  uint32_t code = task.x + 1 < end ? sorted[task.x + 1] : 0u;
-  Fp px, py;
-  ld_aff(&table[code & 0x7fffffffu], px, py);
-  for (uint32_t e = task.x + 1; e < end; ++e) {
-    const uint32_t cur = code;
-    const RFp x = rx_unpack(px);
-    RFp y = rx_unpack(py);
-    if (e + 1 < end) {
-      code = sorted[e + 1];
-      ld_aff(&table[code & 0x7fffffffu], px, py);
-    }
-    if (HAS_INF && table_inf[cur & 0x7fffffffu]) continue;
-    if (cur & 0x80000000u) y = rx_neg_lazy(y);
-    const bool was_inf = g1r_is_inf(acc);
-    G1R r = g1r_madd_lazy_sl(acc, x, y);
-    if (rx_is_zero(r.ZZ)) {  // rare: reload the point rather than keep it live
-      RFp xr, yr;
-      ld_g1r_aff(&table[cur & 0x7fffffffu], xr, yr);
-      if (cur & 0x80000000u) yr = rx_neg(yr);
-      r = g1r_madd_lazy_fix(was_inf, r, xr, yr);
-    }
-    acc = r;
-  }
-  st_g1r(&partials[(size_t)slot * task_stride + pidx], g1r_lazy_finish(acc));
 }
 
 // Bucket sums S_b = sum of bucket b's accumulation partials (task_off[b] .. task_off[b+1]):
@@ -1410,9 +1350,13 @@ static void bitsum_launch(bool wide, uint32_t G, uint32_t slots, uint32_t NR, ui
 
 int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const size_t* lens,
                   const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
-                  hipStream_t stream) {
+                  hipStream_t stream, uint32_t part, uint32_t parts) {
   if (count == 0) return PLK_OK;
   if (count > kMaxSlots) return PLK_E_ARG;
+  if (parts == 0 || (parts & (parts - 1)) || part >= parts) return PLK_E_ARG;
+  // a part's bucket range stays a wide set's (two-level sort, run sums): >= 2^14 buckets
+  if (parts > 1 && (((1u << (s->c - 1)) <= kLdsBuckets) || ((1u << (s->c - 1)) / parts) < (1u << 14)))
+    return PLK_E_ARG;
   size_t max_len = 0, max_tail = 0, total_entries = 0;
   MsmBatch batch{};
   for (size_t k = 0; k < count; ++k) {
@@ -1427,11 +1371,12 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   }
   int st;
   if ((st = ws_reserve(s, w, max_len ? max_len : 1, (uint32_t)count, stream))) return st;
-  const MsmCfg cfg{s->c, s->windows, 1u << (s->c - 1), s->top_shift};
-  const uint32_t B = cfg.B;
+  // B: the buckets this call reduces (all 2^(c-1), or a part's range of them)
+  const uint32_t B_all = 1u << (s->c - 1), B = B_all / parts;
+  const MsmCfg cfg{s->c, s->windows, B, s->top_shift, part * B};
   // wide bucket sets: two-level sort and run-sum reduction; the bit sums then run over the
   // NR = B / 2^rb runs instead of the buckets
-  const bool wide = B > kLdsBuckets;
+  const bool wide = B_all > kLdsBuckets;
   const uint32_t rb = run_bits(B, (uint32_t)count);
   const uint32_t NC = B >> kFineBits, NR = B >> rb;
   const uint32_t G = cdiv(wide ? NR : B, 256);  // a power of two
@@ -1446,8 +1391,8 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   const bool small_batch = !wide && B <= kSortSmallMax && max_len <= kSortOneMax;
   // the task-length floor: kChunkSmall for small batches when the workspace was sized for it
   const uint32_t chunk_floor = small_batch ? std::max(kChunkSmall, w.cap_chunk_min) : kChunkMin;
-  const uint32_t chunk_fit =
-      (uint32_t)std::min<size_t>(kChunkMax, std::max<size_t>(chunk_floor, total_entries / PLK_CHUNK_TARGET));
+  const uint32_t chunk_fit = (uint32_t)std::min<size_t>(
+      kChunkMax, std::max<size_t>(chunk_floor, total_entries / parts / PLK_CHUNK_TARGET));
   const uint32_t chunk = wide && count > 1 ? kChunkMax : chunk_fit;
   const size_t max_tasks_used = (size_t)s->windows * max_len / chunk + B;
   if (max_tasks_used + 1 > w.task_stride) return PLK_E_DEVICE;  // sizing invariant (ws_reserve)
@@ -1562,22 +1507,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   // start / stop events stamped by the dispatch itself (its execution, as rocprofv3 times
   // it), not by the stream: with several lanes on the GPU a stream event would also count
   // the time the kernel waits behind other lanes' kernels
-  {
-    const dim3 grid(cdiv(max_tasks_used, 256), slots), block(256);
-    if (s->has_inf) {
-      hipExtLaunchKernelGGL(k_accumulate<true>, grid, block, 0, stream, w.ev0, w.ev1, 0,
-                            (const uint2*)w.tasks.as<uint2>(), (const uint32_t*)w.task_off.as<uint32_t>(),
-                            B, (uint64_t)w.task_stride, (const uint32_t*)w.sorted.as<uint32_t>(),
-                            (uint64_t)w.sorted_stride, (const G1Affine*)s->table.as<G1Affine>(),
-                            (const uint8_t*)s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
-    } else {
-      hipExtLaunchKernelGGL(k_accumulate<false>, grid, block, 0, stream, w.ev0, w.ev1, 0,
-                            (const uint2*)w.tasks.as<uint2>(), (const uint32_t*)w.task_off.as<uint32_t>(),
-                            B, (uint64_t)w.task_stride, (const uint32_t*)w.sorted.as<uint32_t>(),
-                            (uint64_t)w.sorted_stride, (const G1Affine*)s->table.as<G1Affine>(),
-                            (const uint8_t*)s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
-    }
-  }
+  launch_accumulate(s->has_inf, dim3(cdiv(max_tasks_used, 256), slots), stream, w.ev0, w.ev1,
+                    w.tasks.as<uint2>(), w.task_off.as<uint32_t>(), B, (uint64_t)w.task_stride,
+                    w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride, s->table.as<G1Affine>(),
+                    s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
   if (wide) {
     hipLaunchKernelGGL(k_runsum1, dim3(cdiv(NR, 256), slots), dim3(256), 0, stream,
                        (const uint32_t*)w.task_off.as<uint32_t>(), B, rb, (uint64_t)w.task_stride,
@@ -1655,11 +1588,20 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
       acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + j]));
     }
     if (wide) {  // over the runs: K (sum_r (r + 1) Y_r - sum_r Y_r) + sum_r T_r (k_runsum2)
-      G1xyzz a = rx_to_r_domain(T[(size_t)k * nout + nbits + 1]);
+      const G1xyzz ysum = rx_to_r_domain(T[(size_t)k * nout + nbits + 1]);
+      G1xyzz a = ysum;
       a.Y = fe_neg(a.Y);
       acc = xyzz_add(acc, a);
       for (uint32_t i = 0; i < rb; ++i) acc = xyzz_dbl(acc);
       acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + nbits]));
+      if (cfg.b_lo) {  // a part: its buckets' weights are b_lo + 1 + b', so + b_lo sum_b S_b
+        G1xyzz m = xyzz_infinity();
+        for (int i = 31 - __builtin_clz(cfg.b_lo); i >= 0; --i) {
+          m = xyzz_dbl(m);
+          if ((cfg.b_lo >> i) & 1u) m = xyzz_add(m, ysum);
+        }
+        acc = xyzz_add(acc, m);
+      }
     }
     Fp x, y;
     const bool fin = xyzz_to_affine(acc, x, y);

@@ -28,6 +28,9 @@ constexpr uint32_t kMaxSlots = 16;  // independent MSMs per batch
 struct MsmCfg {
   uint32_t c, W, B;
   uint32_t top_shift;  // plk_srs::top_shift
+  // bucket range of a part (msm_run_batch parts > 1: the wide-set sort keeps only digits of
+  // buckets [b_lo, b_lo + B), renumbered from 0); b_lo = 0 for a whole MSM
+  uint32_t b_lo;
 };
 
 // Kernel-argument view of one batch of independent MSMs (slot = blockIdx.y).
@@ -123,5 +126,12 @@ struct MsmWorkspace {
 };
 
 int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStream_t stream);
+
+// k_accumulate (msm_acc.hip) over grid.x * 256 task lanes per slot (grid.y = slots), stamped
+// with the start / stop events ev0 / ev1 by the dispatch itself
+void launch_accumulate(bool has_inf, dim3 grid, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1,
+                       const uint2* tasks, const uint32_t* task_off, uint32_t B, uint64_t task_stride,
+                       const uint32_t* sorted, uint64_t sorted_stride, const G1Affine* table,
+                       const uint8_t* table_inf, G1xyzz* partials);
 
 }  // namespace plk

@@ -310,18 +310,62 @@ def shard_prover_lane(lane, tau, n_points: int, group=None, device=None, ctx=Non
     return lo, sl
 
 
-class ShardedPlonkParams:
-    """PlonkParams whose G1 powers are spread over the ranks of a process group."""
+def window_bits(n_points: int) -> int:
+    """The MSM window size c the library picks for an SRS of n_points (srs.hip choose_c,
+    without the PLK_MSM_C override)."""
+    return 20 if n_points >= 1 << 20 else 17 if n_points >= 1 << 16 else 15 if n_points >= 1 << 14 else 0
 
-    def __init__(self, k: int, tau, n_points: int | None = None, ctx=None, group=None):
+
+def bucket_parts_ok(n_points: int, parts: int) -> bool:
+    """Whether plk_commit_batch_dev_part accepts `parts` bucket ranges on an SRS of n_points:
+    a power of two, a wide bucket set (c >= 17) and >= 2^14 buckets per part."""
+    import os
+    c = int(os.environ.get("PLK_MSM_C", "0")) or window_bits(n_points)
+    return (parts >= 1 and parts & (parts - 1) == 0 and c >= 17
+            and (1 << (c - 1)) // parts >= 1 << 14)
+
+
+class ShardedPlonkParams:
+    """PlonkParams whose MSM work is spread over the ranks of a process group, two ways:
+
+    * mode "points" (rounds 1-4): the G1 powers are split into contiguous SRS slices, rank r
+      holds slice r (``PlonkParams.setup_range``) and runs the whole Pippenger over its slice
+      of every polynomial. The accumulation divides by G; each rank still sorts into and
+      reduces the FULL bucket set (2^19 buckets at 2^20), a fixed cost that does not shrink.
+    * mode "buckets" (round 5, SURVEY §8e "partial bucket sums for a single large MSM"): every
+      rank holds the whole SRS and window table, reads every scalar, and keeps only the
+      digits of its bucket range [r, r + 1) x 2^(c-1) / G (plk_commit_batch_dev_part): its
+      sort, accumulation AND run-sum / bit-sum reduction cover 1/G of the buckets. The rank's
+      share sum_{b in range} (b + 1) S_b is one point; the shares are all-gathered and folded
+      exactly as the slices' partials are. G must be a power of two with 2^(c-1) / G >=
+      2^14 (c = 20 from 2^20 points: up to 32 ranks; c = 17: up to 4); "auto" takes it then
+      and the point slices otherwise.
+
+    Outputs are identical in both modes (canonical affine, the fold order is irrelevant)."""
+
+    def __init__(self, k: int, tau, n_points: int | None = None, ctx=None, group=None,
+                 mode: str = "points"):
         import torch.distributed as dist
 
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.n = n_points if n_points is not None else (1 << k) + PlonkParams.SLACK
-        self.lo, self.hi = shard_range(self.n, self.world, self.rank)
-        self.local = PlonkParams.setup_range(tau, self.lo, self.hi - self.lo, ctx)
+        if mode not in ("points", "buckets", "auto"):
+            raise ValueError(f"ShardedPlonkParams: mode {mode!r}")
+        if mode in ("buckets", "auto"):
+            ok = bucket_parts_ok(self.n, self.world)
+            if mode == "buckets" and not ok:
+                raise ValueError(f"ShardedPlonkParams: {self.world} bucket ranges need a power-of-"
+                                 f"two world and 2^(c-1) / world >= 2^14 (SRS of {self.n} points)")
+            mode = "buckets" if ok else "points"
+        self.mode = mode
+        if mode == "buckets":
+            self.lo, self.hi = 0, self.n
+            self.local = PlonkParams.setup(k, tau, ctx, n_points=self.n)
+        else:
+            self.lo, self.hi = shard_range(self.n, self.world, self.rank)
+            self.local = PlonkParams.setup_range(tau, self.lo, self.hi - self.lo, ctx)
 
     def _local_spans(self, length: int) -> tuple[int, int]:
         """(offset, length) of this rank's part of a length-`length` polynomial; the last
@@ -333,11 +377,15 @@ class ShardedPlonkParams:
     def commit_batch_dev(self, ptrs_lens, stream: int = 0, device=None):
         """Independent commits of device polynomials [(ptr, len)] (coefficients replicated
         on every rank) -> list of Commitment / PlonkError, identical on every rank."""
-        spans = []
-        for ptr, length in ptrs_lens:
-            off, m = self._local_spans(length)
-            spans.append((ptr + 32 * off, m))
-        part = self.local.commit_batch_dev(spans, stream, raise_on_error=False)
+        if self.mode == "buckets":
+            part = self.local.commit_batch_dev(list(ptrs_lens), stream, raise_on_error=False,
+                                               part=self.rank, parts=self.world)
+        else:
+            spans = []
+            for ptr, length in ptrs_lens:
+                off, m = self._local_spans(length)
+                spans.append((ptr + 32 * off, m))
+            part = self.local.commit_batch_dev(spans, stream, raise_on_error=False)
         words = np.zeros((len(part), 13), dtype=np.uint64)
         sts = []
         for i, p in enumerate(part):
@@ -356,5 +404,5 @@ class ShardedPlonkParams:
         return r
 
 
-__all__ = ["ExchangeService", "ShardedPlonkParams", "gather_fold", "shard_range",
+__all__ = ["ExchangeService", "ShardedPlonkParams", "bucket_parts_ok", "gather_fold", "shard_range",
            "shard_prover_lane", "srs_slice", "torch_allgather", "PLK_E_DEGREE"]

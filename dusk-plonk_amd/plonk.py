@@ -40,6 +40,7 @@ ABI_SYMBOLS = (
     "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
     "plk_srs_len", "plk_srs_points", "plk_msm", "plk_commit", "plk_commit_dev",
     "plk_srs_last_msm_stats", "plk_debug_field_op", "plk_commit_batch_dev",
+    "plk_commit_batch_dev_part",
     "plk_srs_setup_range", "plk_g1_sum", "plk_msm_sharded", "plk_srs_msm_stats_reset",
     "plk_srs_cum_msm_stats", "plk_ntt_stream", "plk_aggregate_witness",
     "plk_aggregate_witness_dev",
@@ -114,6 +115,7 @@ def _lib():
                                              C.POINTER(u32)]),
             "plk_debug_field_op": (i32, [vp, i32, i32, vp, vp, vp, sz]),
             "plk_commit_batch_dev": (i32, [vp, vp, vp, sz, vp, vp, vp]),
+            "plk_commit_batch_dev_part": (i32, [vp, vp, vp, sz, u32, u32, vp, vp, vp]),
             "plk_srs_setup_range": (i32, [vp, vp, u64, sz, vp, pp]),
             "plk_g1_sum": (i32, [vp, sz, vp]),
             "plk_msm_sharded": (i32, [vp, i32, vp, sz, vp]),
@@ -427,16 +429,23 @@ class PlonkParams:
                                      C.c_void_p(stream or None)), "commit_dev")
         return Commitment(out)
 
-    def commit_batch_dev(self, ptrs_lens, stream: int = 0, raise_on_error: bool = True):
+    def commit_batch_dev(self, ptrs_lens, stream: int = 0, raise_on_error: bool = True,
+                         part: int = 0, parts: int = 1):
         """Commit several device-resident polynomials [(ptr, len), ...] as one batch.
-        Returns a list of Commitment (or PlonkError per failed slot when not raising)."""
+        Returns a list of Commitment (or PlonkError per failed slot when not raising).
+        parts > 1: only bucket range `part` of `parts` (plk_commit_batch_dev_part): the
+        returned points are that range's shares, which sum over the parts to the commits."""
         k = len(ptrs_lens)
         ptrs = (C.c_void_p * k)(*[C.c_void_p(p) for p, _ in ptrs_lens])
         lens = (C.c_size_t * k)(*[n for _, n in ptrs_lens])
         outs = np.zeros((k, 13), dtype=np.uint64)
         sts = (C.c_int * k)()
-        st = _lib().plk_commit_batch_dev(self._h, ptrs, lens, k, _ptr(outs), sts,
-                                         C.c_void_p(stream or None))
+        if parts == 1:
+            st = _lib().plk_commit_batch_dev(self._h, ptrs, lens, k, _ptr(outs), sts,
+                                             C.c_void_p(stream or None))
+        else:
+            st = _lib().plk_commit_batch_dev_part(self._h, ptrs, lens, k, part, parts, _ptr(outs),
+                                                  sts, C.c_void_p(stream or None))
         if st not in (PLK_OK, PLK_E_DEGREE) or (raise_on_error and st != PLK_OK):
             raise PlonkError(st, "commit_batch_dev")
         return [Commitment(outs[i]) if sts[i] == PLK_OK else PlonkError(sts[i], "commit")

@@ -138,6 +138,21 @@ int plk_commit_dev(plk_srs* srs, const plk_fr* d_coeffs, size_t len, plk_g1* out
 int plk_commit_batch_dev(plk_srs* srs, const plk_fr* const* d_coeffs, const size_t* lens,
                          size_t count, plk_g1* outs, int* statuses, void* stream);
 
+/* Bucket-range part of plk_commit_batch_dev (round 5; SURVEY §8e, the north star's "partial
+ * bucket sums for a single large MSM"): the same commits, but only the Pippenger buckets of
+ * part `part` of `parts` (parts a power of two): bucket range [part, part + 1) x 2^(c-1) /
+ * parts of the SRS's window size c. outs[k] is that range's share sum_{b in range} (b + 1) S_b
+ * of commit k; the shares of parts 0 .. parts-1 sum (plk_g1_sum) to plk_commit_batch_dev's
+ * outputs. Every part reads all scalars and the whole window table, sorts and accumulates
+ * only its buckets' entries and reduces only its buckets: one GPU per part, each doing
+ * ~1/parts of the accumulation AND of the bucket reduction (the SRS-slice split,
+ * plk_prover_shard / plk_msm_sharded, divides only the accumulation). The degree check runs
+ * in every part (same status everywhere). PLK_E_ARG unless 2^(c-1) > 32768 (a wide bucket
+ * set, c >= 17: SRS >= 2^16 points) and 2^(c-1) / parts >= 2^14. */
+int plk_commit_batch_dev_part(plk_srs* srs, const plk_fr* const* d_coeffs, const size_t* lens,
+                              size_t count, uint32_t part, uint32_t parts, plk_g1* outs,
+                              int* statuses, void* stream);
+
 /* PlonkParams::compute_aggregate_witness(&[p_0..p_(k-1)], &point, &v) (prover.rs:422-438,
  * 444-450): W(X) = (sum_i v^i p_i(X)) / (X - point), the remainder dropped (Ruffini). The
  * k polynomials (d_polys[i], lens[i] coefficients) are device pointers; d_out receives

@@ -275,3 +275,65 @@ def test_msm_tail_forms(plk, gpu_ctx, oracle, monkeypatch, quad, c, logn):
         }
         for name, s in cases.items():
             assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), (name, quad)
+
+
+@pytest.mark.parametrize("c,logn,parts", [(20, 6, 2), (20, 6, 8), (20, 6, 32), (17, 6, 4)])
+def test_msm_bucket_parts_vs_pyref(plk, gpu_ctx, golden, monkeypatch, c, logn, parts):
+    """plk_commit_batch_dev_part: EVERY part's share equals the restated split
+    (oracle/pyref.py msm_bucket_part: same recoding, halving and top-window spread), and the
+    shares fold to the golden MSM. c forced on the golden 64-point SRS (wide bucket sets)."""
+    import torch
+    import pyref as P
+    monkeypatch.setenv("PLK_MSM_C", str(c))
+    g = golden["msm"]
+    pp = plk.PlonkParams.setup(logn, g["tau"], gpu_ctx, n_points=64)
+    pts = P.g1_vec_from_np(g["srs"])
+    for name in ("random", "minus_one", "high_bits"):
+        sc = g[f"{name}_scalars"]
+        d = torch.from_numpy(sc.view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        shares = []
+        for q in range(parts):
+            got = pp.commit_batch_dev([(d.data_ptr(), sc.shape[0])], part=q, parts=parts)[0]
+            if q in (0, 1, parts - 1):  # pyref shares are slow: spot-check three parts
+                want = P.g1_vec_to_np([P.msm_bucket_part(pts, P.fr_vec_from_np(sc), c, q, parts)])[0]
+                assert np.array_equal(got.words, want), (name, q)
+            shares.append(got.words)
+        assert np.array_equal(plk.plonk.g1_sum(np.stack(shares)).words, g[f"{name}_result"]), name
+
+
+def test_msm_bucket_parts_2_20(plk, gpu_ctx):
+    """The bench's configs[2] MSM (2^20 points, c = 20) as 8 bucket-range parts: the folded
+    shares equal the unsharded commit (itself checked against the oracle in
+    test_msm_2_20_vs_oracle); invalid part counts are refused."""
+    import torch
+    k = 20
+    tau = random_fr(1, seed=2020)[0]
+    pp = plk.PlonkParams.setup(k, tau, gpu_ctx)
+    n = 1 << k
+    sc = random_fr(n, seed=4242)
+    d = torch.from_numpy(sc.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    full = pp.commit_batch_dev([(d.data_ptr(), n)])[0]
+    for parts in (2, 8):
+        shares = [pp.commit_batch_dev([(d.data_ptr(), n)], part=q, parts=parts)[0].words
+                  for q in range(parts)]
+        assert np.array_equal(plk.plonk.g1_sum(np.stack(shares)).words, full.words), parts
+    for parts in (3, 64):
+        with pytest.raises(plk.PlonkError) as e:
+            pp.commit_batch_dev([(d.data_ptr(), n)], part=0, parts=parts)
+        assert e.value.status == plk.PLK_E_ARG
+
+
+def test_msm_bucket_parts_degree_error(plk, gpu_ctx, golden, monkeypatch):
+    """A polynomial longer than the SRS fails with PLK_E_DEGREE in every part."""
+    import torch
+    monkeypatch.setenv("PLK_MSM_C", "20")
+    g = golden["msm"]
+    pp = plk.PlonkParams.setup(6, g["tau"], gpu_ctx, n_points=64)
+    bad = np.concatenate([g["random_scalars"], random_fr(9, seed=5)])
+    d = torch.from_numpy(bad.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    for q in range(4):
+        r = pp.commit_batch_dev([(d.data_ptr(), bad.shape[0])], raise_on_error=False, part=q, parts=4)
+        assert isinstance(r[0], plk.PlonkError) and r[0].status == plk.PLK_E_DEGREE

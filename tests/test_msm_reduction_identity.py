@@ -85,3 +85,77 @@ def test_signed_recoding(c):
         assert carry == 0
         assert all(abs(x) <= 1 << (c - 1) for x in d)
         assert sum(x << (w * c) for w, x in enumerate(d)) == s
+
+
+def run_bits_lone(B, run_lanes=65536, kmax=4, kmin=1):
+    """msm.hip run_bits for a lone MSM: the largest rb <= 4 with B >> rb >= 2^16 run lanes."""
+    rb = kmax
+    while rb > kmin and (B >> rb) < run_lanes:
+        rb -= 1
+    return rb
+
+
+def reduce_wide(S):
+    """The wide path's reduction of a bucket array as the kernels + host tail compute it:
+    run sums (k_runsum1/2), bit sums over the runs (k_bitsum1/2), K (sum (r+1) Y_r - sum Y_r)
+    + sum T_r; also returns sum_r Y_r (= sum_b S_b)."""
+    B = len(S)
+    K = 1 << run_bits_lone(B)
+    Y, T = [], []
+    for r in range(B // K):
+        suffix = [sum(S[r * K + t2] for t2 in range(t, K)) for t in range(K)]
+        Y.append(suffix[0])
+        T.append(sum(suffix))
+    return K * (bitsum_device(Y) - sum(Y)) + sum(T), sum(Y)
+
+
+@pytest.mark.parametrize("c,parts", [(17, 2), (17, 4), (18, 8), (20, 8), (20, 32)])
+def test_bucket_parts_identity(c, parts):
+    """msm_run_batch's bucket-range parts (plk_commit_batch_dev_part): part p keeps the digits
+    of buckets [b_lo, b_lo + B/parts), b_lo = p B / parts (k_chist / k_cscatter: b - b_lo
+    unsigned < B/parts, digit 0 wrapping out of range), reduces them as a wide set of B/parts
+    buckets and adds b_lo sum_b S_b on the host; the parts' shares sum to sum_b (b+1) S_b.
+    Integers mod r stand in for the points (the identities are linear): the whole MSM
+    sum_i s_i P_i with the signed recoding, the scalar halving and the spread top window."""
+    rng = random.Random(c * 100 + parts)
+    W = (255 + c - 1) // c
+    tb = 254 - c * (W - 1)
+    ts = c - 1 - tb if 0 <= tb < c - 1 else 0
+    r_mod = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    q = r_mod  # the group order: r P = 0 is what makes the scalar halving exact
+    n = 40
+    P = [rng.randrange(q) for _ in range(n)]
+    sc = [rng.randrange(r_mod) for _ in range(n - 4)] + [0, 1, r_mod - 1, (r_mod - 1) // 2 + 1]
+    B = 1 << (c - 1)
+    inv2ts = pow(1 << ts, -1, q)
+    entries = {}  # bucket -> sum of signed table values
+    for s, p in zip(sc, P):
+        neg = s > (r_mod - 1) // 2
+        h = r_mod - s if neg else s
+        d, carry = digits(h, c, W)
+        assert carry == 0
+        for w, x in enumerate(d):
+            if w == W - 1:
+                x <<= ts  # digit_at scales the top window's digit, its table row is pre-divided
+                tv = pow(2, c * w, q) * inv2ts % q * p % q
+            else:
+                tv = pow(2, c * w, q) * p % q
+            if x == 0:
+                continue
+            assert abs(x) <= B
+            sign = (x < 0) != neg
+            entries[abs(x) - 1] = (entries.get(abs(x) - 1, 0) + (-tv if sign else tv)) % q
+    want = sum(s * p for s, p in zip(sc, P)) % q
+    Bp = B // parts
+    total = 0
+    for part in range(parts):
+        b_lo = part * Bp
+        S = [0] * Bp
+        for b, v in entries.items():
+            bb = (b - b_lo) & 0xFFFFFFFF  # the kernels' unsigned range test
+            if bb < Bp:
+                S[bb] = v
+        local, ssum = reduce_wide(S)
+        assert local == sum((b + 1) * v for b, v in enumerate(S))
+        total += local + b_lo * ssum
+    assert total % q == want

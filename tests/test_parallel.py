@@ -103,6 +103,63 @@ def test_sharded_msm_gather_fold_gloo_world2():
     assert out == {0: True, 1: True}
 
 
+class _FakePartParams:
+    """CPU stand-in for a rank's PlonkParams in ShardedPlonkParams' bucket mode: its
+    commit_batch_dev(part=, parts=) returns the bucket-range shares of the restated split
+    (oracle/pyref.py msm_bucket_part, window c = 20) — `ptr` indexes host scalar arrays."""
+
+    def __init__(self, points, polys, c=20):
+        self.points, self.polys, self.c = points, polys, c
+        self.calls = []
+
+    def commit_batch_dev(self, ptrs_lens, stream=0, raise_on_error=True, part=0, parts=1):
+        import pyref as P
+        import dusk_plonk_amd as plk
+        self.calls.append((part, parts))
+        out = []
+        for ptr, length in ptrs_lens:
+            sc = P.fr_vec_from_np(self.polys[ptr][:length])
+            share = P.msm_bucket_part(self.points[:length], sc, self.c, part, parts)
+            out.append(plk.Commitment(P.g1_vec_to_np([share])[0]))
+        return out
+
+
+def _cpu_bucket_worker(rank, world, port, q):
+    """ShardedPlonkParams.commit_batch_dev in bucket mode over gloo: each rank's share of its
+    bucket range (the restated split), one all-gather, host fold (plk_g1_sum)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tests"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import torch.distributed as dist
+    import pyref as P
+    from dusk_plonk_amd.parallel import ShardedPlonkParams, bucket_parts_ok
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = dict(np.load(ROOT / "tests" / "golden" / "msm_golden.npz", allow_pickle=False))
+        pts = P.g1_vec_from_np(g["srs"])
+        slots = ["random", "minus_one", "sparse"]
+        sh = object.__new__(ShardedPlonkParams)  # no GPU: the rank's params are the fake
+        sh.group, sh.world, sh.rank, sh.mode = None, world, rank, "buckets"
+        sh.lo, sh.hi, sh.n = 0, len(pts), len(pts)
+        sh.local = _FakePartParams(pts, [g[f"{s}_scalars"] for s in slots])
+        res = sh.commit_batch_dev([(i, len(pts)) for i in range(len(slots))])
+        ok = all(np.array_equal(r.words, g[f"{s}_result"]) for r, s in zip(res, slots))
+        ok &= sh.local.calls == [(rank, world)]
+        ok &= bucket_parts_ok(1 << 20, world) and not bucket_parts_ok(1 << 20, 3)
+        ok &= bucket_parts_ok(1 << 16, 4) and not bucket_parts_ok(1 << 16, 8)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_split_gather_fold_gloo_world2():
+    """The bucket-range split of a single MSM on 2 gloo ranks, CPU only."""
+    out = _spawn(_cpu_bucket_worker, 2)
+    assert out == {0: True, 1: True}
+
+
 def _gpu_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, str(ROOT))
