@@ -101,6 +101,9 @@ def parse():
                          "with their own streams, each driven by a host thread. 0 = 12 at "
                          "n >= 2^18, 14 at 2^15..2^17, 16 below (2 HIP hardware queues per "
                          "lane; round-3 sweep tools/gpu_r03_lanes.sh in DESIGN §6)")
+    ap.add_argument("--fit-lanes", action="store_true",
+                    help="prove mode: lower the lanes per GPU (same on every rank) when the "
+                         "warmup's synthesis would need > 90 %% of a rank's CPU share")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4); "
                          "0 = min(32, 2 x lanes): more lanes than queues serialise on them")
@@ -301,27 +304,33 @@ def recheck_proofs(lanes, checker) -> tuple[int, list]:
     return len(lanes), bad
 
 
-def host_core_budget(torch, dist, world, lanes, step_s, device):
-    """Host cores the proof server needs against the cores it has: per rank, each lane's
-    synthesis (measured in the warmup) runs once per step beside the GPU work, so a rank
-    needs lanes x synth_s / step_s cores; summed over the node's ranks and compared with the
-    node's usable cores (affinity mask / cgroup quota). Returns (needed_per_rank,
-    needed_node, available_node) — identical on every rank."""
+def host_core_budget(dist, world, lanes, step_s, share=None) -> dict:
+    """Host cores the proof server needs against the cores it has. Each lane synthesises one
+    fresh witness per step beside the GPU work (synthesis time measured in the warmup), so a
+    rank needs lanes x synth_s / step_s cores. The GPU box gives every GPU its own CPU share
+    (cpu_share: affinity, cgroup quota and the OMP_NUM_THREADS share), so each rank's need is
+    compared with ITS OWN share; `ratio` is the largest need / share over the ranks (the same
+    on every rank), and the per-host sums are reported beside it."""
+    import socket
     ts = [s for ln in lanes for s in ln.synth_all]
     synth = float(np.mean(ts)) if ts else 0.0
     need = len(lanes) * synth / max(step_s, 1e-9)
-    share = cpu_share()
-    avail = share["cgroup_quota_cpus"] or share["affinity"]
-    avail = min(avail, share["affinity"]) if avail else share["affinity"]
-    node = need
+    share = share or cpu_share()
+    avail = float(share["available"])
+    mine = {"host": socket.gethostname(), "need": need, "available": avail}
+    ranks = [mine]
     if world > 1:
-        on = device if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([need, -float(avail)], dtype=torch.float64, device=on)
-        dist.all_reduce(t[:1])
-        m = t[1:].clone()
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)  # the smallest report, negated
-        node, avail = float(t[0].item()), -float(m.item())
-    return need, node, avail
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    hosts = {}
+    for r in ranks:
+        h = hosts.setdefault(r["host"], {"ranks": 0, "need": 0.0, "available": 0.0})
+        h["ranks"] += 1
+        h["need"] += r["need"]
+        h["available"] += r["available"]
+    ratio = max(r["need"] / max(r["available"], 1e-9) for r in ranks)
+    return {"needed_per_rank": need, "available_per_rank": avail, "ratio": ratio,
+            "oversubscribed": ratio > 0.9, "per_host": hosts}
 
 
 def cpu_baseline(k: int, pp, threads: int):
@@ -513,6 +522,29 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=No
     return out
 
 
+def stored_cpu_baseline(k: int, world: int, gpu_value: float):
+    """A multi-rank line's CPU baseline: the STORED measurement of the restated reference
+    prover on one GPU's CPU share (profiles/r03_cpu_node_n20.json: 16 concurrent
+    single-thread 2^20 proofs, tools/cpu_node_n20.py), not re-measured at world > 1 (each
+    rank's host share is busy synthesising its lanes' witnesses). The N-GPU comparison is
+    against N such shares."""
+    f = ROOT / "profiles" / "r03_cpu_node_n20.json"
+    try:
+        d = json.loads(f.read_text())
+    except (OSError, ValueError):
+        return {"source": "stored (unavailable)", "value": None, "unit": "constraints/s"}
+    per_share = d["window_constraints_per_s"]
+    return {"source": f"stored: {f.relative_to(ROOT)} (tools/cpu_node_n20.py, measured on the "
+                      "GPU box)",
+            "kind": "port", "unit": "constraints/s", "n": d.get("n"),
+            "value": per_share * world, "cores": d["procs"] * world,
+            "per_share": {"value": per_share, "cores": d["procs"]},
+            "sample": (f"{d['procs']} concurrent single-thread restated-reference proofs at "
+                       f"n=2^{int(d['n']).bit_length() - 1} per GPU share, x {world} shares"
+                       + ("" if k == 20 else f" (stored at 2^20; this line is 2^{k})")),
+            "ratio": {"gpu_over_cpu_shares": gpu_value / (per_share * world)}}
+
+
 def host_info():
     """nproc, usable cores and the CPU model of the machine the baseline ran on."""
     model = "unknown"
@@ -665,10 +697,13 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
     # node's ranks would need more cores than the node has, prove with fewer lanes per rank
     # rather than oversubscribe (the same count on every rank: the figures are all-reduced)
     warm_step = (time.perf_counter() - tw) / max(1, args.warmup)
-    need, need_node, avail_node = host_core_budget(torch, dist, world, lanes, warm_step, device)
+    hc = host_core_budget(dist, world, lanes, warm_step)
+    # --fit-lanes: prove with fewer lanes (the same count on every rank) when a rank's
+    # synthesis would need more than 90 % of its CPU share; by default the lanes stay as
+    # requested and the line says whether the host was oversubscribed
     L_run = L
-    if args.warmup and need_node > 0.9 * avail_node:
-        L_run = max(1, int(L * 0.9 * avail_node / need_node))
+    if args.fit_lanes and args.warmup and hc["oversubscribed"]:
+        L_run = max(1, int(L * 0.9 / hc["ratio"]))
     active = lanes[:L_run]
     for ln in lanes:
         ln.lane.msm_stats(reset=True)
@@ -730,7 +765,9 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
             "n": n, "log_n": k, "proofs_per_step": proofs,
             "parallelism": (f"msm-shard x{world} x {L} lane(s), partials all-gathered over "
                             f"{transport(dist)}" if shard else
-                            f"proof-batch x{world * L} ({L} concurrent prover lane(s) per GPU)"),
+                            f"proof-batch x{world * L} ({L} concurrent prover lane(s) per GPU)")
+                           + (f"; lanes lowered from {len(lanes_all)} to {L} (--fit-lanes: host "
+                              "CPU share)" if L < len(lanes_all) else ""),
             "msm_window_bits": cbits,
             "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
         },
@@ -741,12 +778,11 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
         "proofs_checked": checked - len(mismatched),
         "proofs_check": ("each lane's last timed proof re-proved alone on one lane after the "
                          "timed region, byte-identical"),
-        "host_cores": {"needed_per_rank": need, "needed_node": need_node,
-                       "available_node": avail_node, "lanes_requested": len(lanes_all),
-                       "lanes_run": L,
-                       "note": "lanes x measured synthesis s / step s (warmup), summed over "
-                               "the node's ranks; lanes are lowered when the node would be "
-                               "oversubscribed"},
+        "host_cores": {**hc, "lanes_requested": len(lanes_all), "lanes_run": L,
+                       "note": "lanes x measured synthesis s / step s (warmup) per rank, against "
+                               "that rank's own CPU share (cpu_share); ratio = the largest "
+                               "need / share over the ranks; lanes are lowered only with "
+                               "--fit-lanes"},
     }
     # roofline of the dominant kernel (k_accumulate, ~60 % of a proof's GPU time) from its
     # solo launches; the in-workload averages beside them
@@ -779,9 +815,20 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
                     "2 MSMs)",
         })
         result["roofline"] = roof
+    if world > 1 and "roofline" in result:
+        # every rank's own k_accumulate figures (its lane 0's solo proof), gathered to the line
+        r = result["roofline"]
+        mine = {"rank": rank, "frac": r["frac"], "point_adds_per_s": r["point_adds_per_s"],
+                "avg_launch_ms": r["avg_launch_ms"], "hbm_gbs": r["hbm"]["achieved"]}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        r["per_rank"] = allr
+        r["note"] += "; per_rank: every rank's own solo figures (top level: rank 0's)"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_full(k, base.pp, cpu_threads(args),
                                                    gpu_value=result["value"])
+    elif rank == 0 and world > 1:
+        result["cpu_baseline"] = stored_cpu_baseline(k, world, result["value"])
     if rank == 0:
         print(json.dumps(result), flush=True)
     for ln in lanes_all:

@@ -602,18 +602,6 @@ PLK_RX void rx_mul_add_mul2(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& c0, c
   rx_prod_group<C, kRxMulAdd, kRxMul, kRxMul>(a, b, c, d, o);
 }
 
-// (a0 b0 + c0 d0, a1 b1)
-template <class C>
-PLK_RX void rx_mul_add_mul(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& c0, const Rx<C>& d0,
-                           const Rx<C>& a1, const Rx<C>& b1, Rx<C>& o0, Rx<C>& o1) {
-  const Rx<C>* a[2] = {&a0, &a1};
-  const Rx<C>* b[2] = {&b0, &b1};
-  const Rx<C>* c[2] = {&c0, &c0};
-  const Rx<C>* d[2] = {&d0, &d0};
-  Rx<C>* o[2] = {&o0, &o1};
-  rx_prod_group<C, kRxMulAdd, kRxMul>(a, b, c, d, o);
-}
-
 // a + b mod 2p-range: [0, 2p) + [0, 2p) -> [0, 2p)
 template <class C>
 PLK_RX Rx<C> rx_add(const Rx<C>& a, const Rx<C>& b) {

@@ -132,72 +132,46 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
 //   * P == 0 (same x): ZZ3 = ZZ1 * P^2 == 0, and then X3 = R^2 + 6p, so R == 0 (same
 //     point: the sum is a doubling) <=> X3 == 0 mod p; otherwise the sum is infinity.
 // A zero ZZ3 is the single (rare) trigger; g1r_madd_lazy_fix finishes those cases.
-#ifndef PLK_MADD_GROUPED
-#define PLK_MADD_GROUPED 1
-#endif
+// GROUPED: the nine reductions as independent groups whose chains interleave (ffr.hpp
+// rx_prod_group): (U2, S2), (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3) — 4 346 VALU + ~440 s_nop per
+// addition; at 2 waves per SIMD (prover lanes) 6.83-6.90e9 solo additions/s in the 2^20 proof
+// against 6.57-6.60e9 for the plain chains at 3 waves (round 5, profiles/r05_acc_dma_ab.jsonl).
+// Otherwise one product at a time (4 536 VALU, no s_nop, ~30 fewer VGPRs): at 3 waves per SIMD
+// it is the faster form where the chip is otherwise idle (lone 2^20 MSM 2.84-2.85 against
+// 2.92 ms). Measured and dropped in round 5: (PPP, Q, ZZ3) + (Y3, ZZZ3) (round 4's libplk-g2)
+// and (PPP, ZZ3) + (Q, ZZZ3) + Y3 alone, both spilling at 3 waves.
+template <bool GROUPED>
 __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, const RFp& y2) {
-#if PLK_MADD_GROUPED == 2
-  // round-4 experiment, rebuilt in round 5 to find the libplk-g2 abort: (U2, S2), (PP, R^2),
-  // (PPP, Q, ZZ3), (Y3, ZZZ3)
-  RFp U2, S2, PP, RR, PPP, Q;
-  rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
-  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
-  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
-  rx_sqr2(P, R, PP, RR);
-  G1R r;
-  rx_mul3(P, PP, p.X, PP, p.ZZ, PP, PPP, Q, r.ZZ);
-  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
-  rx_mul_add_mul(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP,
-                 p.ZZZ, PPP, r.Y, r.ZZZ);
-  return r;
-#elif PLK_MADD_GROUPED == 3
-  // pairs chosen for the smallest live set (3 waves per SIMD): (U2, S2), (PP, R^2),
-  // (PPP, ZZ3), (Q, ZZZ3), then Y3 alone
-  RFp U2, S2, PP, RR, PPP, Q;
-  rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
-  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
-  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
-  rx_sqr2(P, R, PP, RR);
-  G1R r;
-  rx_mul2(P, PP, p.ZZ, PP, PPP, r.ZZ);
-  rx_mul2(p.X, PP, p.ZZZ, PPP, Q, r.ZZZ);
-  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
-  r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP);
-  return r;
-#elif PLK_MADD_GROUPED
-  // the same nine reductions as independent groups whose chains interleave (ffr.hpp
-  // rx_prod_group): (U2, S2), (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3). (PPP, Q, ZZ3) then
-  // (Y3, ZZZ3) compiled to 402 instead of 536 s_nop but issued at the same rate (6.58-6.61e9
-  // against 6.56-6.62e9 additions/s, profiles/r04_madd_grouping_ab.txt): not kept.
-  RFp U2, S2, PP, RR, PPP, Q;
-  rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
-  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
-  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
-  rx_sqr2(P, R, PP, RR);
-  G1R r;
-  rx_mul2(P, PP, p.X, PP, PPP, Q);
-  r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
-  rx_mul_add_mul2(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP,
-                  p.ZZ, PP, p.ZZZ, PPP, r.Y, r.ZZ, r.ZZZ);
-  return r;
-#else
-  const RFp U2 = rx_mul(x2, p.ZZ);
-  const RFp S2 = rx_mul(y2, p.ZZZ);
-  const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);  // (2p, 12p): U2 - X1 in (-8p, 2p)
-  const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);   // (2p, 8p): S2 - Y1 in (-4p, 2p)
-  const RFp PP = rx_sqr(P);
-  const RFp PPP = rx_mul(P, PP);
-  const RFp Q = rx_mul(p.X, PP);
-  G1R r;
-  r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
-  // Y3 = R (Q - X3) + (5p - Y1) PPP with one reduction (all operands normalised, the
-  // split columns of rx_mul_add keep each accumulator below 2^64); value
-  // (8p * 12p + 5p * 2p) / R' + p < 2p at R' = 2^390
-  r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP);
-  r.ZZ = rx_mul(p.ZZ, PP);
-  r.ZZZ = rx_mul(p.ZZZ, PPP);
-  return r;
-#endif
+  if constexpr (GROUPED) {
+    RFp U2, S2, PP, RR, PPP, Q;
+    rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
+    const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
+    const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
+    rx_sqr2(P, R, PP, RR);
+    G1R r;
+    rx_mul2(P, PP, p.X, PP, PPP, Q);
+    r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
+    rx_mul_add_mul2(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP,
+                    p.ZZ, PP, p.ZZZ, PPP, r.Y, r.ZZ, r.ZZZ);
+    return r;
+  } else {
+    const RFp U2 = rx_mul(x2, p.ZZ);
+    const RFp S2 = rx_mul(y2, p.ZZZ);
+    const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);  // (2p, 12p): U2 - X1 in (-8p, 2p)
+    const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);   // (2p, 8p): S2 - Y1 in (-4p, 2p)
+    const RFp PP = rx_sqr(P);
+    const RFp PPP = rx_mul(P, PP);
+    const RFp Q = rx_mul(p.X, PP);
+    G1R r;
+    r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
+    // Y3 = R (Q - X3) + (5p - Y1) PPP with one reduction (all operands normalised, the
+    // split columns of rx_mul_add keep each accumulator below 2^64); value
+    // (8p * 12p + 5p * 2p) / R' + p < 2p at R' = 2^390
+    r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP);
+    r.ZZ = rx_mul(p.ZZ, PP);
+    r.ZZZ = rx_mul(p.ZZZ, PPP);
+    return r;
+  }
 }
 
 // The result of p + (x2, y2) when g1r_madd_lazy_sl returned r with r.ZZ == 0; was_inf =
@@ -219,7 +193,7 @@ __device__ __forceinline__ G1R g1r_madd_lazy_fix(bool was_inf, const G1R& r, con
 // both halves, for callers that keep (x2, y2) live (y2 may be the lazy negation)
 __device__ __forceinline__ G1R g1r_madd_lazy(const G1R& p, const RFp& x2, const RFp& y2) {
   const bool was_inf = g1r_is_inf(p);
-  G1R r = g1r_madd_lazy_sl(p, x2, y2);
+  G1R r = g1r_madd_lazy_sl<true>(p, x2, y2);
   if (rx_is_zero(r.ZZ)) r = g1r_madd_lazy_fix(was_inf, r, x2, rx_canon(y2));
   return r;
 }
@@ -242,7 +216,6 @@ __device__ __forceinline__ G1R g1r_lazy_finish(const G1R& p) {
 // exceptional cases (either operand at infinity, equal x) all give ZZ3 = ZZ1 ZZ2 P^2 = 0 and
 // are repaired after, by g1r_add_lazy.
 __device__ __forceinline__ G1R g1r_add_lazy_sl(const G1R& p, const G1R& q) {
-#if PLK_MADD_GROUPED
   // interleaved groups (ffr.hpp rx_prod_group): (U1, U2, ZZ1 ZZ2), (S1, S2, ZZZ1 ZZZ2),
   // (PP, R^2), (PPP, Q), (Y3, ZZ3, ZZZ3)
   RFp U1, U2, ZZ12, S1, S2, ZZZ12, PP, RR, PPP, Q;
@@ -257,25 +230,6 @@ __device__ __forceinline__ G1R g1r_add_lazy_sl(const G1R& p, const G1R& q) {
   rx_mul_add_mul2(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), S1), PPP,
                   ZZ12, PP, ZZZ12, PPP, r.Y, r.ZZ, r.ZZZ);
   return r;
-#else
-  // ordered so that the operands die early: X1, X2 after P, Y1, Y2 after R, the Z's after
-  // their products
-  const RFp U1 = rx_mul(p.X, q.ZZ);
-  const RFp P = rx_sub_u<FpCfg, 3>(rx_mul(q.X, p.ZZ), U1);  // U2 - U1 + 3p in (p, 5p)
-  const RFp S1 = rx_mul(p.Y, q.ZZZ);
-  const RFp R = rx_sub_u<FpCfg, 3>(rx_mul(q.Y, p.ZZZ), S1);  // S2 - S1 + 3p in (p, 5p)
-  const RFp ZZ12 = rx_mul(p.ZZ, q.ZZ);
-  const RFp ZZZ12 = rx_mul(p.ZZZ, q.ZZZ);
-  const RFp PP = rx_sqr(P);
-  const RFp PPP = rx_mul(P, PP);
-  const RFp Q = rx_mul(U1, PP);
-  G1R r;
-  r.ZZ = rx_mul(ZZ12, PP);
-  r.ZZZ = rx_mul(ZZZ12, PPP);
-  r.X = rx_sub2_n<FpCfg, 6>(rx_sqr(R), PPP, Q);  // R^2 + 6p - PPP - 2Q in (0, 8p)
-  r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), S1), PPP);
-  return r;
-#endif
 }
 
 // dbl-2008-s-1 on a lazy operand (X < 8p, Y < 4p, ZZ, ZZZ < 2p; normalised limbs) with the

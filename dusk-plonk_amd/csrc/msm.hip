@@ -422,15 +422,11 @@ __global__ void __launch_bounds__(1024) k_sort_small(uint32_t* __restrict__ bloc
 // order of the entries inside a bucket differs from the multi-workgroup sort; the bucket's
 // sum (exact XYZZ arithmetic, canonical affine result) does not.
 // Measured (profiles/r04_sortone_runsum_shoup_ab.jsonl, one box, interleaved): 2^12 proofs
-// 7.48 / 7.84 against 7.05 / 7.45 M constraints/s with PLK_SORT_ONE=0.
-// Round 4, opt-in (PLK_SORT_ONE_BIG, measured no faster): also the 2^14-size proofs' commits
-// (c = 15: 2^14 buckets, ~2^14 scalars per slot), whose multi-workgroup sort is five dispatches
-// per batch (k_hist, k_block_scan, k_scan_buckets, k_scatter, k_make_tasks): KEEP = false
-// re-reads the scalars for the scatter instead of holding them in registers.
-constexpr uint32_t kSortOneMax = 8192;            // KEEP: scalars per slot held in registers
-constexpr uint32_t kSortOneBigMax = 1u << 15;     // !KEEP: scalars per slot
-constexpr uint32_t kSortOneBuckets = 16384;       // LDS counters (64 KiB)
-template <bool KEEP>
+// 7.48 / 7.84 against 7.05 / 7.45 M constraints/s with the multi-dispatch sort.
+// Round 4 also measured the 2^14-size proofs' commits (c = 15: 2^14 buckets, ~2^14 scalars
+// per slot) through one workgroup re-reading the scalars for the scatter: no faster
+// (profiles/r04_sort_one_big_ab.jsonl; removed in round 5).
+constexpr uint32_t kSortOneMax = 8192;  // scalars per slot held in registers
 __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, uint64_t n_srs,
                                                    uint32_t chunk, uint32_t* __restrict__ sorted,
                                                    uint64_t sorted_stride,
@@ -438,7 +434,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
                                                    uint32_t* __restrict__ task_off,
                                                    uint2* __restrict__ tasks, uint64_t task_stride,
                                                    uint32_t* __restrict__ flag, uint32_t gen) {
-  __shared__ uint32_t s_count[KEEP ? kSortSmallMax : kSortOneBuckets];
+  __shared__ uint32_t s_count[kSortSmallMax];
   __shared__ uint32_t s_c[1024], s_t[1024], s_f[1024], s_len[kChunkMax], s_cur[kChunkMax];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, nt = 1024, B = cfg.B;  // blockDim.x
   const uint32_t len = batch.len[slot];
@@ -455,7 +451,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   __syncthreads();
   // this thread's scalars (i = tid + k nt, at most kSortOneMax / 1024 of them), brought to
   // [0, (r-1)/2] once and kept in registers for both passes
-  constexpr uint32_t kPer = KEEP ? kSortOneMax / 1024 : 1;
+  constexpr uint32_t kPer = kSortOneMax / 1024;
   Fr sv[kPer];
   bool sneg[kPer];
   auto hist_digits = [&](const Fr& x) {
@@ -465,23 +461,16 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
       if (d != 0) atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
     }
   };
-  if constexpr (KEEP) {
 #pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t i = tid + k * nt;
-      sneg[k] = false;
-      if (i < len) sv[k] = scalar_half(&sc[i], sneg[k]);
-    }
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = tid + k * nt;
+    sneg[k] = false;
+    if (i < len) sv[k] = scalar_half(&sc[i], sneg[k]);
+  }
 #pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {  // histogram of every digit of the slot
-      if (tid + k * nt >= len) break;
-      hist_digits(sv[k]);
-    }
-  } else {
-    for (uint32_t i = tid; i < len; i += nt) {
-      bool neg;
-      hist_digits(scalar_half(&sc[i], neg));
-    }
+  for (uint32_t k = 0; k < kPer; ++k) {  // histogram of every digit of the slot
+    if (tid + k * nt >= len) break;
+    hist_digits(sv[k]);
   }
   __syncthreads();
   // offsets / task offsets / full-task offsets over each thread's contiguous buckets, the
@@ -546,19 +535,11 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
       }
     }
   };
-  if constexpr (KEEP) {
 #pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter, one workgroup)
-      const uint32_t i = tid + k * nt;
-      if (i >= len) break;
-      scatter_digits(sv[k], sneg[k], i);
-    }
-  } else {
-    for (uint32_t i = tid; i < len; i += nt) {
-      bool neg;
-      const Fr x = scalar_half(&sc[i], neg);
-      scatter_digits(x, neg, i);
-    }
+  for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter, one workgroup)
+    const uint32_t i = tid + k * nt;
+    if (i >= len) break;
+    scatter_digits(sv[k], sneg[k], i);
   }
 }
 
@@ -878,13 +859,11 @@ __device__ __forceinline__ G1R shfl_tree(G1R acc, uint32_t e, uint32_t w) {
   return acc;
 }
 
-// QUAD (PLK_BITSUM_QUAD): every "lane" of the reduction trees (k_bucket_sum, k_bitsum1/2) is a quad of 4 lanes holding the same
-// values, adding with g1r_add_quad (g1r.hpp: one product per lane, ~3.5 products issued per
-// addition instead of ~15) — these trees are a chain of dependent additions on a few waves,
-// so their time is one wave's issue of each level. Shuffles move by whole quads.
-#ifndef PLK_BITSUM_QUAD
-#define PLK_BITSUM_QUAD 1
-#endif
+// QUAD: every "lane" of the reduction trees (k_bucket_sum, k_bitsum1/2) is a quad of 4 lanes
+// holding the same values, adding with g1r_add_quad (g1r.hpp: one product per lane, ~3.5
+// products issued per addition instead of ~15) — these trees are a chain of dependent
+// additions on a few waves, so their time is one wave's issue of each level. Shuffles move by
+// whole quads. Which form a batch takes: MsmWorkspace::tail_quad.
 template <bool QUAD>
 struct TailUnit {
   static constexpr uint32_t S = QUAD ? 4 : 1;  // lanes per unit
@@ -907,11 +886,8 @@ struct TailUnit {
   }
 };
 
-// k_bitsum1: the branching addition at two waves per SIMD (2 workgroups of 256 per CU: a lone
-// 2^20 MSM's 512 groups in one round instead of two)
-#ifndef PLK_BITSUM_LAZY
-#define PLK_BITSUM_LAZY 0
-#endif
+// k_bitsum1: the branching addition (single-lane form) at two waves per SIMD (2 workgroups of
+// 256 per CU: a lone 2^20 MSM's 512 groups in one round instead of two)
 #ifndef PLK_BITSUM_WAVES
 #define PLK_BITSUM_WAVES 2
 #endif
@@ -1057,7 +1033,7 @@ __global__ void __launch_bounds__(bitsum1_threads(Z, QUAD), PLK_BITSUM_WAVES) k_
   constexpr bool SPLIT = Z && QUAD;  // two workgroups per group (bitsum1_threads)
   constexpr uint32_t NSU = 4, MEM = 16 / NSU;  // units per sum, members per unit
   constexpr uint32_t NU = bitsum1_threads(Z, QUAD) / TailUnit<QUAD>::S;  // units
-  constexpr bool LZ = PLK_BITSUM_LAZY;
+  constexpr bool LZ = false;
   __shared__ G1xyzz sh[NS];
   const uint32_t slot = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
   const uint32_t role = SPLIT ? blockIdx.z : 0;
@@ -1156,10 +1132,7 @@ __global__ void __launch_bounds__(bitsum1_threads(Z, QUAD), PLK_BITSUM_WAVES) k_
 // Also the batch's readback record (ReadbackHeader): workgroup (0, slot) copies the slot's
 // entry count (its point additions, offsets[B]) next to the flags k_any_nonzero stamped, so
 // the host reads flags, counts and bit sums with ONE copy.
-// k_bitsum2's additions: lazy (PLK_BITSUM2_LAZY=1) or the branching g1r_add
-#ifndef PLK_BITSUM2_LAZY
-#define PLK_BITSUM2_LAZY 1
-#endif
+// k_bitsum2's additions: lazy (the branching g1r_add measured no faster, round 2)
 // QUAD: 128 units of 4 lanes (8 waves, 2 per SIMD: the quad addition's ~250 VGPRs)
 constexpr uint32_t kBitsum2Units(bool quad) { return quad ? 128 : 256; }
 template <bool QUAD>
@@ -1169,7 +1142,7 @@ __global__ void __launch_bounds__(QUAD ? 512 : 256) k_bitsum2(const G1xyzz* __re
                                                  const uint32_t* __restrict__ offsets, uint32_t B,
                                                  uint32_t* __restrict__ entries) {
   constexpr uint32_t UPW = QUAD ? 16 : 64;  // units per wave
-  constexpr bool LZ = PLK_BITSUM2_LAZY || QUAD;
+  constexpr bool LZ = true;
   __shared__ G1xyzz sh[16];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, j = blockIdx.x;
   const TailUnit<QUAD> T(tid);
@@ -1380,6 +1353,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   const uint32_t rb = run_bits(B, (uint32_t)count);
   const uint32_t NC = B >> kFineBits, NR = B >> rb;
   const uint32_t G = cdiv(wide ? NR : B, 256);  // a power of two
+  if (parts > 1 && NR != 256u * G) return PLK_E_DEVICE;  // the part offset's Horner seed below
   const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
   const uint32_t nout = nbits + (wide ? 2u : 0u);         // + sum_r T_r, sum_r Y_r
   const uint32_t slots = (uint32_t)count;
@@ -1410,17 +1384,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   }
   const uint32_t gen = w.gen;
   // small batches: the whole sort (and the degree check) in one dispatch per batch
-#ifndef PLK_SORT_ONE
-#define PLK_SORT_ONE 1
-#endif
-#ifndef PLK_SORT_ONE_BIG  // opt-in: 2^14 proofs 14.8-15.3 against 15.1-15.2 M constraints/s
-#define PLK_SORT_ONE_BIG 0  // without it (profiles/r04_sort_one_big_ab.jsonl): the dispatches saved
-#endif                      // do not pay for one workgroup sorting ~280 K digits per commit
-  // KEEP form for small batches; the re-reading form up to 2^14 buckets / 2^15 scalars for
-  // batches of several commits (one workgroup per slot: a lone commit keeps the
-  // multi-workgroup sort, whose latency is lower)
-  const bool sort_one_big = !wide && count > 1 && B <= kSortOneBuckets && max_len <= kSortOneBigMax;
-  const bool sort_one = PLK_SORT_ONE && (small_batch || (PLK_SORT_ONE_BIG && sort_one_big));
+  const bool sort_one = small_batch;
   if (max_tail && !sort_one) {
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
                        batch, hdr_dev->flag, gen);
@@ -1453,17 +1417,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        (const uint32_t*)w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>(),
                        w.task_off.as<uint32_t>(), w.tasks.as<uint2>(), (uint64_t)w.task_stride);
   } else if (sort_one) {
-    if (small_batch) {
-      hipLaunchKernelGGL(k_sort_one<true>, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
-                         (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
-                         w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
-                         (uint64_t)w.task_stride, hdr_dev->flag, gen);
-    } else {
-      hipLaunchKernelGGL(k_sort_one<false>, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
-                         (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
-                         w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
-                         (uint64_t)w.task_stride, hdr_dev->flag, gen);
-    }
+    hipLaunchKernelGGL(k_sort_one, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
+                       (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
+                       w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
+                       (uint64_t)w.task_stride, hdr_dev->flag, gen);
   } else {
     const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
     if (max_len) {
@@ -1499,15 +1456,14 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                          w.tasks.as<uint2>(), (uint64_t)w.task_stride);
     }
   }
-  const char* quad_env = getenv("PLK_TAIL_QUAD");  // read per batch: tests flip it
   // 0: single-lane trees, 1: quad trees, 2: quad k_bitsum2 only (its few workgroups are
-  // latency-bound at any load)
-  const int tail = !PLK_BITSUM_QUAD ? 0 : quad_env ? atoi(quad_env) : w.tail_quad;
+  // latency-bound at any load); chosen when the workspace is made (msm_common.hpp)
+  const int tail = w.tail_quad;
   const bool quad = tail == 1;
   // start / stop events stamped by the dispatch itself (its execution, as rocprofv3 times
   // it), not by the stream: with several lanes on the GPU a stream event would also count
   // the time the kernel waits behind other lanes' kernels
-  launch_accumulate(s->has_inf, dim3(cdiv(max_tasks_used, 256), slots), stream, w.ev0, w.ev1,
+  launch_accumulate(s->has_inf, !w.shared_chip, dim3(cdiv(max_tasks_used, 256), slots), stream, w.ev0, w.ev1,
                     w.tasks.as<uint2>(), w.task_off.as<uint32_t>(), B, (uint64_t)w.task_stride,
                     w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride, s->table.as<G1Affine>(),
                     s->table_inf.as<uint8_t>(), w.partials.as<G1xyzz>());
@@ -1583,25 +1539,26 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     // host tail: sum_j 2^j T_j (Horner), then canonical affine. The device stages work in
     // the R' domain (ffr.hpp) with values in [0, 2p): reduce and map back to R first.
     G1xyzz acc = xyzz_infinity();
+    // a part (b_lo = part B = part NR K, NR = 2^nbits runs): its buckets weigh b_lo + 1 + b',
+    // i.e. + b_lo sum_b S_b = K 2^nbits part sum_r Y_r — part sum_r Y_r seeds the Horner
+    // below, whose nbits doublings and the K below scale it
+    if (wide && part) {
+      const G1xyzz ysum = rx_to_r_domain(T[(size_t)k * nout + nbits + 1]);
+      for (int i = 31 - __builtin_clz(part); i >= 0; --i) {
+        acc = xyzz_dbl(acc);
+        if ((part >> i) & 1u) acc = xyzz_add(acc, ysum);
+      }
+    }
     for (int j = (int)nbits - 1; j >= 0; --j) {
       acc = xyzz_dbl(acc);
       acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + j]));
     }
     if (wide) {  // over the runs: K (sum_r (r + 1) Y_r - sum_r Y_r) + sum_r T_r (k_runsum2)
-      const G1xyzz ysum = rx_to_r_domain(T[(size_t)k * nout + nbits + 1]);
-      G1xyzz a = ysum;
+      G1xyzz a = rx_to_r_domain(T[(size_t)k * nout + nbits + 1]);
       a.Y = fe_neg(a.Y);
       acc = xyzz_add(acc, a);
       for (uint32_t i = 0; i < rb; ++i) acc = xyzz_dbl(acc);
       acc = xyzz_add(acc, rx_to_r_domain(T[(size_t)k * nout + nbits]));
-      if (cfg.b_lo) {  // a part: its buckets' weights are b_lo + 1 + b', so + b_lo sum_b S_b
-        G1xyzz m = xyzz_infinity();
-        for (int i = 31 - __builtin_clz(cfg.b_lo); i >= 0; --i) {
-          m = xyzz_dbl(m);
-          if ((cfg.b_lo >> i) & 1u) m = xyzz_add(m, ysum);
-        }
-        acc = xyzz_add(acc, m);
-      }
     }
     Fp x, y;
     const bool fin = xyzz_to_affine(acc, x, y);

@@ -8,12 +8,15 @@
 // written packed. Replaces the bucket accumulation of msm_curve_addition inside zksnarks
 // PlonkParams::commit (called at prover.rs:133-136,194,262-265,440,452).
 //
-// The next entry's point is loaded one addition ahead. PLK_ACC_DMA = 1 (round 5): through
-// LDS-DMA (global_load_lds_dwordx4: 6 per 96-B point, no VGPR destination) into a per-wave
+// The next entry's point is loaded one addition ahead (round 5): through LDS-DMA (global_load_lds_dwordx4: 6 per 96-B point, no VGPR destination) into a per-wave
 // staging slot [6][64] x 16 B (6 KiB per wave), read back with ds_read_b128 when its
-// addition starts. The register prefetch (PLK_ACC_DMA = 0, rounds 1-4) held the packed
-// point (24 VGPRs) live through the ~4 900-instruction addition; without it the kernel fits
-// PLK_ACC_WAVES waves per SIMD.
+// addition starts. The register prefetch of rounds 1-4 held the packed
+// point (24 VGPRs) live through the ~4 900-instruction addition: 208 -> 190 VGPRs (grouped
+// products), 173 -> 164 (plain chains, which then fit 3 waves per SIMD without spills), and
+// 438 instead of 547 s_nop per addition. Measured (round 5, one box, interleaved, A/B against
+// the round-4 register prefetch): solo additions/s in the 2^20 proof 5.84-5.87e9 -> 6.83-6.90e9,
+// 2^20 proofs 29.7-30.1 -> 31.6 M constraints/s, lone 2^20 MSM 3.08-3.11 -> 2.92 ms (2.84 in the
+// LONE form).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -21,12 +24,6 @@
 #include "msm_common.hpp"
 #include "g1r.hpp"
 
-#ifndef PLK_ACC_DMA
-#define PLK_ACC_DMA 1
-#endif
-#ifndef PLK_ACC_WAVES
-#define PLK_ACC_WAVES 2  // waves per SIMD the register allocator must fit
-#endif
 
 namespace plk {
 
@@ -34,7 +31,6 @@ namespace {
 
 constexpr uint32_t kAccThreads = 256;
 
-#if PLK_ACC_DMA
 typedef __attribute__((address_space(3))) void lds_void;
 
 // Issue the 6 LDS-DMA loads of one affine point (96 B) into this wave's staging slot:
@@ -59,22 +55,23 @@ __device__ __forceinline__ void unstage_point(const uint4 (*stage)[64], uint32_t
   x = rx_unpack(px);
   y = rx_unpack(py);
 }
-#endif
 
-template <bool HAS_INF>
+// LONE: the form for a chip the MSM has to itself (lone commits, plk_prove's default
+// prover): plain product chains at 3 waves per SIMD; otherwise (prover lanes, several proofs
+// sharing the chip) the interleaved product groups at 2 (g1r.hpp g1r_madd_lazy_sl; round 5
+// A/B, profiles/r05_acc_dma_ab.jsonl)
+template <bool HAS_INF, bool LONE>
 __global__ void __launch_bounds__(kAccThreads)
-    __attribute__((amdgpu_waves_per_eu(PLK_ACC_WAVES, PLK_ACC_WAVES)))
+    __attribute__((amdgpu_waves_per_eu(LONE ? 3 : 2, LONE ? 3 : 2)))
     k_accumulate(const uint2* __restrict__ tasks, const uint32_t* __restrict__ task_off, uint32_t B,
                  uint64_t task_stride, const uint32_t* __restrict__ sorted, uint64_t sorted_stride,
                  const G1Affine* __restrict__ table, const uint8_t* __restrict__ table_inf,
                  G1xyzz* __restrict__ partials) {
   const uint32_t slot = blockIdx.y;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-#if PLK_ACC_DMA
   __shared__ uint4 s_stage[kAccThreads / 64][6][64];
   uint4 (*stage)[64] = s_stage[threadIdx.x >> 6];
   const uint32_t lane = threadIdx.x & 63;
-#endif
   if (t >= task_off[(size_t)slot * (B + 1) + B]) return;
   const uint2 tk = tasks[(size_t)slot * task_stride + t];
   const uint2 task = make_uint2(tk.x, (tk.y >> kTaskShift) + 1);  // first entry, length (>= 1)
@@ -94,7 +91,6 @@ __global__ void __launch_bounds__(kAccThreads)
       acc.ZZZ = rx_one<FpCfg>();
     }
   }
-#if PLK_ACC_DMA
   // entry e's point is in the staging slot when its iteration starts (the compiler waits
   // for the DMA, vmcnt, before the ds_reads); `code` is entry e's index, `next` entry
   // e + 1's, loaded one addition ahead like the point itself; the infinity flag travels
@@ -118,23 +114,9 @@ __global__ void __launch_bounds__(kAccThreads)
       if (e + 2 < end) next = sorted[e + 2];
     }
     if (HAS_INF && cur_inf) continue;
-#else
-  uint32_t code = task.x + 1 < end ? sorted[task.x + 1] : 0u;
-  Fp px, py;
-  ld_aff(&table[code & 0x7fffffffu], px, py);
-  for (uint32_t e = task.x + 1; e < end; ++e) {
-    const uint32_t cur = code;
-    const RFp x = rx_unpack(px);
-    RFp y = rx_unpack(py);
-    if (e + 1 < end) {
-      code = sorted[e + 1];
-      ld_aff(&table[code & 0x7fffffffu], px, py);
-    }
-    if (HAS_INF && table_inf[cur & 0x7fffffffu]) continue;
-#endif
     if (cur & 0x80000000u) y = rx_neg_lazy(y);
     const bool was_inf = g1r_is_inf(acc);
-    G1R r = g1r_madd_lazy_sl(acc, x, y);
+    G1R r = g1r_madd_lazy_sl<!LONE>(acc, x, y);
     if (rx_is_zero(r.ZZ)) {  // rare: reload the point rather than keep it live
       RFp xr, yr;
       ld_g1r_aff(&table[cur & 0x7fffffffu], xr, yr);
@@ -148,17 +130,22 @@ __global__ void __launch_bounds__(kAccThreads)
 
 }  // namespace
 
-void launch_accumulate(bool has_inf, dim3 grid, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1,
-                       const uint2* tasks, const uint32_t* task_off, uint32_t B, uint64_t task_stride,
-                       const uint32_t* sorted, uint64_t sorted_stride, const G1Affine* table,
-                       const uint8_t* table_inf, G1xyzz* partials) {
+void launch_accumulate(bool has_inf, bool lone, dim3 grid, hipStream_t stream, hipEvent_t ev0,
+                       hipEvent_t ev1, const uint2* tasks, const uint32_t* task_off, uint32_t B,
+                       uint64_t task_stride, const uint32_t* sorted, uint64_t sorted_stride,
+                       const G1Affine* table, const uint8_t* table_inf, G1xyzz* partials) {
   const dim3 block(kAccThreads);
-  if (has_inf)
-    hipExtLaunchKernelGGL(k_accumulate<true>, grid, block, 0, stream, ev0, ev1, 0, tasks, task_off, B,
-                          task_stride, sorted, sorted_stride, table, table_inf, partials);
-  else
-    hipExtLaunchKernelGGL(k_accumulate<false>, grid, block, 0, stream, ev0, ev1, 0, tasks, task_off, B,
-                          task_stride, sorted, sorted_stride, table, table_inf, partials);
+#define PLK_ACC_LAUNCH(I, L)                                                                   \
+  hipExtLaunchKernelGGL((k_accumulate<I, L>), grid, block, 0, stream, ev0, ev1, 0, tasks, task_off, \
+                        B, task_stride, sorted, sorted_stride, table, table_inf, partials)
+  if (has_inf) {
+    if (lone) PLK_ACC_LAUNCH(true, true);
+    else PLK_ACC_LAUNCH(true, false);
+  } else {
+    if (lone) PLK_ACC_LAUNCH(false, true);
+    else PLK_ACC_LAUNCH(false, false);
+  }
+#undef PLK_ACC_LAUNCH
 }
 
 }  // namespace plk

@@ -1,5 +1,7 @@
 // msm_common.hpp — device load/store helpers and the per-SRS MSM workspace.
 #pragma once
+#include <cstdlib>
+
 #include "internal.hpp"
 
 namespace plk {
@@ -114,11 +116,25 @@ struct MsmWorkspace {
   uint32_t cap_chunk_min = kChunkMin;  // the task-length floor the buffers were sized for
   // the bit-sum trees' additions: 1 quad-cooperative (g1r_add_quad, lower latency, the lone
   // call's choice), 0 one lane each (fewer issue slots per addition, for prover lanes that
-  // share the chip with other proofs), 2 quads in k_bitsum2 only; PLK_TAIL_QUAD overrides
-  // (experiments)
+  // share the chip with other proofs), 2 quads in k_bitsum2 only (lane_tail_policy).
+  // PLK_TAIL_QUAD (experiments, tests) forces a form for every workspace created while it is
+  // set: read once here, never per batch (a getenv in the hot path raced the tests' setenv)
   int tail_quad = 1;
+  bool tail_forced = false;
+  // the chip is shared with other proofs' kernels (prover lanes): k_accumulate's grouped form
+  // at 2 waves per SIMD; otherwise (lone commits, plk_prove) the LONE form (msm_acc.hip)
+  bool shared_chip = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   MsmStats stats;
+  MsmWorkspace() {
+    if (const char* e = getenv("PLK_TAIL_QUAD")) {
+      const int v = atoi(e);
+      if (v >= 0 && v <= 2) {
+        tail_quad = v;
+        tail_forced = true;
+      }
+    }
+  }
   ~MsmWorkspace() {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -127,11 +143,31 @@ struct MsmWorkspace {
 
 int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStream_t stream);
 
+// The reduction trees' form for a prover lane of an n-row circuit (plk_prover_create; lone
+// commits and plk_prove's default prover keep 1). A lane shares the chip with other lanes'
+// proofs, so issue slots per addition count more than a tree level's latency, except where
+// the reduction tails stay latency-bound. Measured, prover lanes at the bench's lane counts,
+// interleaved on one box (constraints/s, 0 / 1 / 2):
+//   2^12  7.61-7.80 / 8.26-8.65 / —          -> 1 (profiles/r04_tail_quad_ab.jsonl, r04p)
+//   2^14  15.1-15.6 / 15.2-15.5 / +3 %        -> 2 (profiles/r04_tail_mode2_ab.jsonl,
+//                                                   r04_tail_modes_small_ab.jsonl)
+//   2^16  26.2-26.9 / 24.1-26.2 / -3 % vs 0   -> 0
+//   2^20  32.5-32.7 / 32.1-32.3 / +0.6 % vs 0 -> 2
+// 2^15, 2^17 and 2^18 follow their neighbours' row (0: both neighbours of 2^17 / 2^18 prefer
+// the single-lane trees or gain < 1 % from quads, and 2^15 sits between 2^14's tie and
+// 2^16's 0); 2^19 and up as 2^20.
+inline int lane_tail_policy(uint64_t n) {
+  if (n <= (1ull << 13)) return 1;
+  if (n == (1ull << 14)) return 2;
+  if (n >= (1ull << 19)) return 2;
+  return 0;
+}
+
 // k_accumulate (msm_acc.hip) over grid.x * 256 task lanes per slot (grid.y = slots), stamped
 // with the start / stop events ev0 / ev1 by the dispatch itself
-void launch_accumulate(bool has_inf, dim3 grid, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1,
-                       const uint2* tasks, const uint32_t* task_off, uint32_t B, uint64_t task_stride,
-                       const uint32_t* sorted, uint64_t sorted_stride, const G1Affine* table,
-                       const uint8_t* table_inf, G1xyzz* partials);
+void launch_accumulate(bool has_inf, bool lone, dim3 grid, hipStream_t stream, hipEvent_t ev0,
+                       hipEvent_t ev1, const uint2* tasks, const uint32_t* task_off, uint32_t B,
+                       uint64_t task_stride, const uint32_t* sorted, uint64_t sorted_stride,
+                       const G1Affine* table, const uint8_t* table_inf, G1xyzz* partials);
 
 }  // namespace plk

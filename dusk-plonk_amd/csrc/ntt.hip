@@ -60,55 +60,16 @@ constexpr int kL = RxShape<FrCfg>::L;
 constexpr uint32_t kDS = 1u << kMaxLe;
 constexpr uint32_t kDSSmall = 256;
 
-// -DPLK_NTT_FUSE=1: the first radix-4 step on the loaded registers (k_ntt_pass), one LDS
-// round trip fewer per pass. Parity-green, measured within noise (2^20 6.85 / 6.89, 2^23
-// 8.48 / 8.37 G points/s fused / not, tools/gpu_ntt_ab.sh) and 131 VGPRs (3 waves per SIMD
-// instead of the 4 the LDS allows; capped at 128 it spills and runs 3 % slower): off
-#ifndef PLK_NTT_FUSE
-#define PLK_NTT_FUSE 0
-#endif
-constexpr bool kFuseFirstStep = PLK_NTT_FUSE != 0;
-// -DPLK_NTT_R2FIRST=0: odd-radix passes end in a stage of half 1 of their own (round 2 form)
-#ifndef PLK_NTT_R2FIRST
-#define PLK_NTT_R2FIRST 1
-#endif
-constexpr bool kR2First = PLK_NTT_R2FIRST != 0;
-// -DPLK_NTT_R4FIRST=1: even-radix passes run their first radix-4 step in the input loop (127
-// VGPRs, parity-green; measured 2^20 dft + idft 0.309-0.312 against 0.302-0.304 ms, 2^23 and
-// proofs within noise, profiles/r03_ntt_r4first_ab.txt): off
-#ifndef PLK_NTT_R4FIRST
-#define PLK_NTT_R4FIRST 0
-#endif
-constexpr bool kR4First = PLK_NTT_R4FIRST != 0;
-// The last two radix-4 steps of a pass (halves 8, 4 then 2, 1) exchange data only inside
-// 16-row blocks of one column, between the 4 groups (t, 16B + r), r < 4. PLK_NTT_QUADX puts
-// those 4 groups on the 4 lanes of a quad (group index r lowest) and: 1 = exchanges through
-// LDS without the workgroup barrier (the producer and consumer lanes are in one wave);
-// 2 = exchanges in registers (DPP quad transpose, quad_transpose) with no LDS round trip;
-// 0 = off (one barrier and LDS round trip per step). Measured (profiles/r04_ntt_quadx_ab.jsonl,
-// one box, interleaved, dft + idft per step): 2^20 0.3078-0.3079 / 0.3028-0.3033 / 0.2981-0.3058
-// ms, 2^23 2.095-2.099 / 2.083-2.086 / 2.045-2.048 ms, 2^17 within noise, 2^20 proofs
-// 31.6-32.0 / 32.5-32.7 / 32.3-32.9 M constraints/s: the DPP exchange (+13 % VALU cycles in
-// the loop body) still beats the LDS round trip and barrier it removes. Default 2.
-#ifndef PLK_NTT_QUADX
-#define PLK_NTT_QUADX 2
-#endif
-// The radix-4 step's four products as interleaved chains (ffr.hpp rx_prod_group, round 4):
-// nonzero = two pairs (default; round 4 also measured a triple (y2, y3, o1) then o3 alone),
-// 0 = one by one (round 3). Loop VALU cycles 4 137 (one by one) -> 3 914 (triple) / 3 865
-// (pairs); measured dft + idft per step, 2^20:
-// 0.299-0.301 / 0.292-0.297 / 0.291-0.299 ms, 2^23: 2.036-2.045 / 2.007-2.015 / 1.987-1.996 ms
-// (profiles/r04_ntt_grouped_ab.jsonl; proofs within noise)
-#ifndef PLK_NTT_GROUPED
-#define PLK_NTT_GROUPED 2
-#endif
+// Measured and removed in round 5 (git history): the first radix-4 step on the
+// loaded registers (round 2, within noise, 131 VGPRs), the first radix-4 step of even-radix
+// passes in the input loop (round 3, slower), the persistent software-pipelined pass with
+// register prefetch (round 3, slower at 2 and 3 waves per SIMD), the last two steps' quad
+// exchange through LDS (round 4, between the barrier form and the DPP form kept below), the
+// radix-4 products one by one (round 4, slower than the pairs kept below) and the
+// constant-twiddle Shoup product (round 4, slower).
 // k_ntt_pass minimum waves per SIMD (-DPLK_NTT_MINW=4 caps it at 128 VGPRs)
 #ifndef PLK_NTT_MINW
 #define PLK_NTT_MINW 1
-#endif
-// the persistent variant's (PF): its prefetched loads stay live across the butterflies
-#ifndef PLK_NTT_PF_MINW
-#define PLK_NTT_PF_MINW 2
 #endif
 
 // Element idx of a data plane sits at word idx ^ ((idx / 32) * 9 mod 32): ds_read_b32 /
@@ -236,38 +197,16 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
   return r;
 }
 
-// Products by the inner (stage) twiddles staged in LDS. PLK_NTT_SHOUP: the table holds
-// (w, w' = floor(w 2^261 / r)) planes and the product is the constant-operand Shoup form
-// (ffr.hpp fr_shoup, 143 mads, output < 3r); otherwise Montgomery by w R' (rx_mul, < 2r).
-// Measured (round 4, profiles/r04_sortone_runsum_shoup_ab.jsonl, parity-green with the NTT
-// and prover tests): dft + idft per step 2^20 0.310-0.313 against 0.298-0.302 ms, 2^23
-// 2.171-2.174 against 2.097-2.121 ms — SLOWER. As compiled, the last low column's 18 products
-// become v_mul_lo_u32 (only their low bits count), the small constants of 2^261 - r become
-// multiply / shift sequences and LLVM splits the chains with 64-bit merge adds: 472 mads +
-// 96 v_mul_lo_u32 against 612 mads, the same VALU cycles per loop body, and a standalone
-// product rate 1.15-1.25e11 against 1.31-1.40e11 /s (tools/ubench_shoup.hip). Off.
-#ifndef PLK_NTT_SHOUP
-#define PLK_NTT_SHOUP 0
-#endif
-constexpr uint32_t kTwPlanes = PLK_NTT_SHOUP ? 2 : 1;  // twiddle plane sets in LDS
+// Products by the inner (stage) twiddles staged in LDS: Montgomery by w R' (rx_mul, < 2r);
+// two at once as interleaved chains (ffr.hpp rx_prod_group, round 4: loop VALU cycles
+// 4 137 -> 3 865, dft + idft per step 2^20 0.299-0.301 -> 0.291-0.299 ms, 2^23 2.04 -> 1.99 ms,
+// profiles/r04_ntt_grouped_ab.jsonl).
 __device__ __forceinline__ RFr twmul(const RFr& a, const uint32_t* twl, uint32_t TS, uint32_t idx) {
-#if PLK_NTT_SHOUP
-  return fr_shoup(a, lds_ld(twl, TS, idx), lds_ld(twl + kL * TS, TS, idx));
-#else
   return rx_mul(a, lds_ld(twl, TS, idx));
-#endif
 }
 __device__ __forceinline__ void twmul2(const RFr& a0, uint32_t i0, const RFr& a1, uint32_t i1,
                                        const uint32_t* twl, uint32_t TS, RFr& o0, RFr& o1) {
-#if PLK_NTT_SHOUP
-  o0 = fr_shoup(a0, lds_ld(twl, TS, i0), lds_ld(twl + kL * TS, TS, i0));
-  o1 = fr_shoup(a1, lds_ld(twl, TS, i1), lds_ld(twl + kL * TS, TS, i1));
-#elif PLK_NTT_GROUPED
   rx_mul2(a0, lds_ld(twl, TS, i0), a1, lds_ld(twl, TS, i1), o0, o1);
-#else
-  o0 = rx_mul(a0, lds_ld(twl, TS, i0));
-  o1 = rx_mul(a1, lds_ld(twl, TS, i1));
-#endif
 }
 
 // Two radix-2 DIF stages (halves 2h and h) on rows x0..x3 = j, j+h, j+2h, j+3h of one
@@ -293,7 +232,7 @@ __device__ __forceinline__ void r4_math(const uint32_t* twl, uint32_t TS, const 
     // straight-line code leaves three independent products (y2, y3, output 1) to
     // interleave. Stage of half h: twiddle w^(r s2) for both pairs; outputs normalised.
     // The step's products go as interleaved pairs (twmul2: ffr.hpp rx_prod_group, no 64-bit
-    // merge add per column) unless PLK_NTT_GROUPED = 0. Products < 2r (< 3r with Shoup).
+    // merge add per column). Products < 2r.
     RFr y2, y3;
     twmul2(rx_sub_u<FrCfg, 6>(x0, x2), r << sh1, rx_sub_u<FrCfg, 6>(x1, x3), (r + h) << sh1, twl, TS,
            y2, y3);
@@ -348,8 +287,8 @@ __device__ __forceinline__ void quad_transpose(RFr& a0, RFr& a1, RFr& a2, RFr& a
 // with x_(j+R/8) = 0 except for j = 0 — the 8n coset transforms of the prover's
 // (n + small)-coefficient polynomials. They are computed directly from the loaded rows
 // (7 multiplies per row instead of three stages of butterflies over 8x the rows).
-template <int PRE, int POST, int PRUNE, uint32_t DS, bool PF>
-__global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
+template <int PRE, int POST, int PRUNE, uint32_t DS>
+__global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                   const Fr* __restrict__ tw,
                                                   const Fr* __restrict__ ptw,
                                                   const Fr* __restrict__ pre,
@@ -363,7 +302,7 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   const uint32_t TS = PRUNE ? R : H;
   uint32_t* data = smem32;          // kL planes of E (stride DS >= E)
   uint32_t* twl = smem32 + kL * DS;
-  uint32_t* ztab = twl + kTwPlanes * kL * TS;  // kZTab (reduce_q)
+  uint32_t* ztab = twl + kL * TS;  // kZTab (reduce_q)
 
   // vector blockIdx.y of a batch: its input, output and scale-table rows (NttBatch::group)
   {
@@ -378,16 +317,7 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   const uint32_t nr_log = log_n - lr;  // log2(N/R)
 
-  for (uint32_t x = tid; x < TS; x += bd) {
-#if PLK_NTT_SHOUP
-    RFr w, wp;
-    fr_shoup_prep(ld_rfr(&tw[(size_t)x << nr_log]), w, wp);
-    lds_st(twl, TS, x, w);
-    lds_st(twl + kL * TS, TS, x, wp);
-#else
-    lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
-#endif
-  }
+  for (uint32_t x = tid; x < TS; x += bd) lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
   for (uint32_t x = tid; x < kQMax * kL; x += bd) ztab[x] = kZTab.v[x];
 
   // every load of the thread's (at most kLoadIt, E / bd <= 4) elements is issued before the
@@ -417,36 +347,17 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
       }
     }
   };
-  // PF (persistent, software-pipelined; opt-in, PLK_NTT_PF): the grid holds fewer workgroups
-  // than tiles and each takes tiles blockIdx.x, + gridDim.x, ...; the next tile's loads are
-  // issued as soon as the current tile's inputs sit in LDS, so they run under its
-  // butterflies and stores (a lone transform's tiles otherwise all load, compute and store in
-  // lockstep). Measured slower (round 3, tools/gpu_r03_pf*.sh, dft + idft per step): 2^20
-  // 0.305 ms off / 0.332 at 512 workgroups (2 waves per SIMD, 204 VGPRs) / 0.35 at 768 (3
-  // waves, 168 VGPRs + spills); 2^23 1.94 / 2.35 / 2.37 — the registers that carry the next
-  // tile's loads cost more occupancy than the overlap returns.
-  const uint32_t nblk = 1u << (log_n - lr - lt);
-  uint32_t tile = blockIdx.x;
-  if (PF) issue(tile << lt);
-  for (;;) {
-  const uint32_t i0 = tile << lt;
+  const uint32_t i0 = blockIdx.x << lt;
 
   // radix-2 stages left: the first radix-4 step's half is 2^(lh-1) (three stages done in
   // closed form when pruning)
   int lh = (int)lr - 1 - (PRUNE ? 3 : 0);
-  // first radix-4 step fused into the load phase (uniform): a thread's four elements form
-  // one of its groups when E = 4 bd
-  const bool fuse = kFuseFirstStep && !PRUNE && lr >= 2 && E == 4 * bd && !(lr & 1);
   // odd radix: the first radix-2 stage (half R/2) runs on the loaded registers — a thread's
   // elements c and c + nit/2 are rows j and j + R/2 of one column when E >= 2 bd — and the
   // remaining even count of stages ends in the twiddle-free radix-4 step of halves (2, 1),
   // instead of a last stage of half 1 in its own LDS round trip (one round trip and barrier
   // fewer, R/4 fewer products per column)
-  const bool r2first = !PRUNE && kR2First && (lr & 1) && lr >= 3 && E >= 2 * bd;
-  // even radix, E = 4 bd: a thread's four elements are one group of the first radix-4 step
-  // (rows j + c R/4); the last one meets the other three, read back from the thread's own
-  // LDS slots, and the step runs in the input loop (no registers held across the loads)
-  const bool r4first = !PRUNE && kR4First && !fuse && !(lr & 1) && lr >= 4 && E == 4 * bd;
+  const bool r2first = !PRUNE && (lr & 1) && lr >= 3 && E >= 2 * bd;
   if (PRUNE) {
     __syncthreads();
     // item = (row j < R/8, column t, half hs): blocks 4 hs .. 4 hs + 3 of (j, t)
@@ -469,19 +380,14 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q) {
         const uint32_t blk = 4 * hs + q, b = bitrev(blk, 3);
-#if PLK_NTT_SHOUP  // rx_add wants [0, 2r): the Shoup products (< 3r) go through reduce_q
-        RFr v = (j == 0 || b == 0) ? x : reduce_q(twmul(x, twl, TS, j * b), ztab);
-        if (has8) v = rx_add(v, b == 0 ? x8 : reduce_q(twmul(x8, twl, TS, R8 * b), ztab));
-#else
         RFr v = (j == 0 || b == 0) ? x : rx_mul(x, lds_ld(twl, TS, j * b));
         if (has8) v = rx_add(v, b == 0 ? x8 : rx_mul(x8, lds_ld(twl, TS, R8 * b)));
-#endif
         lds_std<DS>(data, ((blk * R8 + j) << lt) + t, v);
       }
     }
   }
   if (!PRUNE) {
-    if (!PF) issue(i0);
+    issue(i0);
     auto input = [&](uint32_t c) -> RFr {  // element tid + c bd, pre-scaled / twiddled
       const uint32_t e = tid + c * bd;
       const uint32_t t = e & (T - 1), j = e >> lt;
@@ -497,47 +403,29 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
       if (PRE != 1 && lp != 0) v = rx_mul(v, rx_unpack(aux[c]));
       return v;
     };
-    if (fuse) {
-      // E = 4 bd: the thread's elements are rows j, j + R/4, j + R/2, j + 3R/4 of column t
-      // (j = tid >> lt < R/4) — exactly one group of the first radix-4 step (halves R/2 and
-      // R/4), which therefore runs on the loaded registers: one LDS round trip fewer
-      __syncthreads();  // twl / ztab staged
-      const uint32_t t = tid & (T - 1), j = tid >> lt, h = R >> 2;
-      const RFr x0 = input(0), x1 = input(1), x2 = input(2), x3 = input(3);
-      r4_step<DS>(data, twl, TS, ztab, j, h, 0, 1, (j << lt) + t, ((j + h) << lt) + t,
-                  ((j + 2 * h) << lt) + t, ((j + 3 * h) << lt) + t, x0, x1, x2, x3);
-      lh -= 2;
-    } else {
+    {
       // element e = tid + c bd sits at LDS index e = (row << lt) + column. With r2first the
       // upper half's elements (c >= nit / 2: rows j + R/2) meet their partner, which this
       // thread stored at e - E/2 one iteration earlier (read back without a barrier), and the
       // pair's butterfly is stored in place. One loop for both forms: as two code paths the
       // compiler hoisted all four inputs above the branch (137 VGPRs instead of 115)
-      if (r2first || r4first) __syncthreads();  // twl / ztab staged
+      if (r2first) __syncthreads();  // twl / ztab staged
 #pragma unroll
       for (uint32_t c = 0; c < kLoadIt; ++c) {
         if (c >= nit) break;
         const uint32_t e = tid + c * bd;
         const RFr v = input(c);  // < 2r, normalised
-        if (r4first && c == 3) {
-          const uint32_t t = tid & (T - 1), j = tid >> lt, h = R >> 2;
-          const RFr x0 = lds_ldd<DS>(data, e - 3 * bd), x1 = lds_ldd<DS>(data, e - 2 * bd);
-          const RFr x2 = lds_ldd<DS>(data, e - bd);
-          r4_step<DS>(data, twl, TS, ztab, j, h, 0, 1, (j << lt) + t, ((j + h) << lt) + t,
-                      ((j + 2 * h) << lt) + t, ((j + 3 * h) << lt) + t, x0, x1, x2, v);
-        } else if (r2first && 2 * c >= nit) {
+        if (r2first && 2 * c >= nit) {
           const uint32_t el = e - (E >> 1);
           const RFr a = lds_ldd<DS>(data, el);
           lds_std<DS>(data, el, reduce_q(add_u(a, v), ztab));                        // < 1.6r
-          lds_std<DS>(data, e, twmul(sub_u(a, v), twl, TS, el >> lt));  // < 2r (3r Shoup)
+          lds_std<DS>(data, e, twmul(sub_u(a, v), twl, TS, el >> lt));  // < 2r
         } else if (e < E) {
           lds_std<DS>(data, e, v);
         }
       }
       if (r2first) lh -= 1;
-      if (r4first) lh -= 2;
     }
-    if (PF && tile + gridDim.x < nblk) issue((tile + gridDim.x) << lt);  // next tile's loads
   }
   __syncthreads();
 
@@ -548,10 +436,13 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
   for (; lh >= 1; lh -= 2) {
     const uint32_t h = 1u << (lh - 1);
     const uint32_t sh1 = lr - 1 - lh, sh2 = lr - lh;  // twiddle index shifts of both stages
-    // the last two steps with their groups of a 16-row block on one quad (PLK_NTT_QUADX)
-    const bool quad = PLK_NTT_QUADX != 0 && (lh == 3 || lh == 1) && lr >= 5 &&
-                      (E >> 2) % bd == 0;
-    if (PLK_NTT_QUADX == 2 && quad && lh == 3) {
+    // the last two radix-4 steps (halves 8, 4 then 2, 1) exchange data only inside 16-row
+    // blocks of one column, between the 4 groups (t, 16B + r), r < 4: with those groups on the
+    // 4 lanes of a quad (r lowest) the exchange is a DPP quad transpose in registers, with no
+    // LDS round trip and no barrier (round 4: dft + idft 2^20 0.308 -> 0.298-0.306 ms, 2^23
+    // 2.10 -> 2.05 ms, profiles/r04_ntt_quadx_ab.jsonl)
+    const bool quad = lh == 3 && lr >= 5 && (E >> 2) % bd == 0;
+    if (quad) {
       // halves 8 and 4, quad transpose in registers, halves 2 and 1: one LDS round trip
       for (uint32_t g = tid; g < (E >> 2); g += bd) {
         const uint32_t r = g & 3u, t = (g >> 2) & (T - 1), B = g >> (2 + lt);
@@ -571,14 +462,7 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
       continue;
     }
     for (uint32_t g = tid; g < (E >> 2); g += bd) {
-      uint32_t t, jg;
-      if (quad) {  // r lowest: the 4 groups of a (column, 16-row block) on one quad
-        t = (g >> 2) & (T - 1);
-        jg = ((g >> (2 + lt)) << 2) + (g & 3u);
-      } else {
-        t = g & (T - 1);
-        jg = g >> lt;
-      }
+      const uint32_t t = g & (T - 1), jg = g >> lt;
       const uint32_t r = jg & (h - 1);
       const uint32_t j = ((jg >> (lh - 1)) << (lh + 1)) + r;
       const uint32_t i0 = (j << lt) + t, i1 = ((j + h) << lt) + t;
@@ -587,14 +471,7 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
       const RFr x2 = lds_ldd<DS>(data, i2), x3 = lds_ldd<DS>(data, i3);
       r4_step<DS>(data, twl, TS, ztab, r, h, sh1, sh2, i0, i1, i2, i3, x0, x1, x2, x3);
     }
-    if (PLK_NTT_QUADX == 1 && quad && lh == 3) {
-      // the next step reads only what this wave's own quads wrote: LDS writes of a wave are
-      // visible to its lanes once they complete — no workgroup barrier
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      __builtin_amdgcn_wave_barrier();
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
   }
   if (lh == 0) {  // odd radix: last stage of half 1 (twiddle-free)
     for (uint32_t b = tid; b < (E >> 1); b += bd) {
@@ -626,11 +503,6 @@ __global__ void __launch_bounds__(256, PF ? PLK_NTT_PF_MINW : PLK_NTT_MINW) k_nt
     else if (POST == 2) v = rx_mul(v, ld_rfr(&post[pos]));
     else v = reduce_q(v, ztab);  // < 1.6r
     st_fr(&out[pos], rx_pack_canonical(v));
-  }
-  if (!PF) break;
-  tile += gridDim.x;
-  if (tile >= nblk) break;
-  __syncthreads();  // the output reads of this tile before the next tile's LDS stores
   }
 }
 
@@ -854,17 +726,9 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     // (round 3: an LDS floor of 54 / 80 KB per workgroup, i.e. 2 - 3 resident workgroups per
     // CU so that a lone transform's tiles run in staggered generations, measured 3 - 7 %
     // slower at 2^20 and 2^23: the lost occupancy costs more than the overlap gains)
-    const size_t lds = ((size_t)(small ? kDSSmall : kDS) +
-                        kTwPlanes * ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
+    const size_t lds = ((size_t)(small ? kDSSmall : kDS) + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
                        kL * sizeof(uint32_t);
-    // persistent software-pipelined passes (k_ntt_pass PF): a lone large transform's grid of
-    // pf_grid workgroups, each taking blocks / pf_grid tiles (PLK_NTT_PF = the grid size, 0 off)
-    static const uint32_t pf_grid = [] {
-      const char* e = getenv("PLK_NTT_PF");
-      return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    const bool pf = pf_grid > 0 && !prune && !small && count == 1 && blocks > pf_grid;
-    dim3 grid(pf ? pf_grid : blocks, count);
+    dim3 grid(blocks, count);
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
     NttStrides str;
@@ -875,21 +739,20 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     str.in_group = first && !no_input ? bt.in_group_stride : 0;
     str.group_in = first ? bt.group : 0;
     str.group_post = last ? bt.group : 0;
-#define PLK_LAUNCH_DS(PRE, POST, PRUNE, DS, PF)                                           \
+#define PLK_LAUNCH_DS(PRE, POST, PRUNE, DS)                                               \
   do {                                                                                    \
-    const void* kp_ = reinterpret_cast<const void*>(&k_ntt_pass<PRE, POST, PRUNE, DS, PF>); \
+    const void* kp_ = reinterpret_cast<const void*>(&k_ntt_pass<PRE, POST, PRUNE, DS>);   \
     if (lds > 65536)                                                                      \
       PLK_HIP_TRY(hipFuncSetAttribute(kp_, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
-    hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE, DS, PF>), grid, dim3(bd), lds, stream, src, dst, \
+    hipLaunchKernelGGL((k_ntt_pass<PRE, POST, PRUNE, DS>), grid, dim3(bd), lds, stream, src, dst, \
                        tw, ptw, pre_table ? pre_table : d->coset_pow.as<Fr>(),            \
                        bt.post ? bt.post : d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n,  \
                        ps.lp, ps.lr, ps.lt, lin, str);                                     \
   } while (0)
 #define PLK_LAUNCH(PRE, POST, PRUNE)                              \
   do {                                                            \
-    if (small) PLK_LAUNCH_DS(PRE, POST, PRUNE, kDSSmall, false);   \
-    else if (!PRUNE && pf) PLK_LAUNCH_DS(PRE, POST, 0, kDS, true); \
-    else PLK_LAUNCH_DS(PRE, POST, PRUNE, kDS, false);             \
+    if (small) PLK_LAUNCH_DS(PRE, POST, PRUNE, kDSSmall);          \
+    else PLK_LAUNCH_DS(PRE, POST, PRUNE, kDS);                     \
   } while (0)
     if (prune) {
       if (pre == 1) PLK_LAUNCH(1, 0, 1);

@@ -916,9 +916,6 @@ int plk_key_info(const plk_key* key, uint64_t* n, uint64_t* m, plk_g1* commitmen
 }
 
 // ----------------------------------------------------------------------- prover
-#ifndef PLK_LANE_QUAD_MAX_LOG
-#define PLK_LANE_QUAD_MAX_LOG 13
-#endif
 int plk_prover_create(plk_key* key, plk_prover** out) {
   try {
     if (!key || !out) return PLK_E_ARG;
@@ -927,15 +924,10 @@ int plk_prover_create(plk_key* key, plk_prover** out) {
     std::unique_ptr<plk_prover> p(new plk_prover());
     p->key = key;
     p->ws = msm_workspace_new();
-    // a lane shares the chip with other lanes' proofs: its bit sums use the single-lane
-    // additions (fewer issue slots) except for small circuits, whose proofs stay bound by
-    // their reduction chains' latency (msm_common.hpp tail_quad; the default prover of
-    // plk_prove and lone commits keep the quad form)
-    // 2^14 and 2^19 up: quads in k_bitsum2 only (2^14 proofs +3 % over either other form,
-    // 2^20 +0.6 %, three interleaved runs each; 2^16 -3 %: profiles/r04_tail_mode2_ab.jsonl,
-    // r04_tail_modes_small_ab.jsonl; 2^12: full quads, +10 %)
-    const uint64_t n = key->n;
-    p->ws->tail_quad = n <= (1ull << PLK_LANE_QUAD_MAX_LOG) ? 1 : (n == (1ull << 14) || n >= (1ull << 19)) ? 2 : 0;
+    // a lane shares the chip with other lanes' proofs: the reduction trees' form by circuit
+    // size (msm_common.hpp lane_tail_policy, with the measured rows)
+    if (!p->ws->tail_forced) p->ws->tail_quad = lane_tail_policy(key->n);
+    p->ws->shared_chip = true;
     PLK_HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->own_stream = true;
     *out = p.release();

@@ -324,7 +324,11 @@ int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int ra
  * limbs >= the modulus, and finite points not on y^2 = x^3 + 4. The identity (ASSUMED
  * encoding) is written as x = 0, y = 0, is_infinity = 1; decode takes is_infinity = 1 with
  * (x, y) = (0, 0) or zkcrypto's (0, one) as the identity and returns it as (0, 0, 1); other
- * coordinates under the flag are rejected. */
+ * coordinates under the flag are rejected. DELIBERATE DIVERGENCE (parity unpinned): a
+ * derived SCALE Decode plus zkcrypto's flag-only is_identity would accept ANY (x, y) under
+ * is_infinity = 1 as the identity; this decoder is strict so that one proof has one byte
+ * string (a verifier hashing proof bytes sees no malleable identity encodings). No fixture
+ * in the reference covers either behaviour. */
 #define PLK_PROOF_SCALE_BYTES (11 * 97 + 16 * 32)
 int plk_proof_encode(const plk_proof* proof, uint8_t* out, size_t cap, size_t* len);
 int plk_proof_decode(const uint8_t* in, size_t len, plk_proof* proof);

@@ -140,3 +140,70 @@ def test_shard_msm_world1_over_rccl():
     check_contract(d, 2, 1)
     assert d["scaling"] == "strong" and "RCCL" in d["config"]["parallelism"]
     assert d["proofs_checked"] == 2
+
+
+class _Lane:
+    def __init__(self, synth):
+        self.synth_all = synth
+
+
+def _budget_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 0: 12 lanes x 0.05 s synthesis per 0.4 s step = 1.5 cores of a 16-core share;
+        # rank 1: 12 x 0.5 / 0.4 = 15 cores of a 16-core share (oversubscribed at > 90 %)
+        share = {"available": 16}
+        lanes = [_Lane([0.05 if rank == 0 else 0.5])] * 12
+        hc = bench.host_core_budget(dist, world, lanes, 0.4, share=share)
+        ok = abs(hc["needed_per_rank"] - (1.5 if rank == 0 else 15.0)) < 1e-9
+        ok &= hc["available_per_rank"] == 16
+        ok &= abs(hc["ratio"] - 15.0 / 16) < 1e-9 and hc["oversubscribed"]
+        host = next(iter(hc["per_host"].values()))
+        ok &= host["ranks"] == 2 and abs(host["need"] - 16.5) < 1e-9 and host["available"] == 32
+        # a node of 8 GPUs at ~2.5 cores each against 16-core shares: not oversubscribed
+        # (round 4 compared the node's sum with ONE share and would have cut lanes to ~8)
+        hc2 = bench.host_core_budget(dist, world, [_Lane([0.083])] * 12, 0.4, share=share)
+        ok &= not hc2["oversubscribed"]
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_core_budget_per_rank_share_gloo_world2():
+    """each rank's synthesis need is compared with its own CPU share (the GPU box
+    gives every GPU one), not the node's summed need with one share."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_budget_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    out = dict(q.get(timeout=5) for _ in range(2))
+    assert out == {0: True, 1: True}
+    for p in procs:
+        assert p.exitcode == 0
+
+
+@pytest.mark.gpu
+def test_prove_line_world2_self_describing():
+    """A multi-rank prove line (2 ranks sharing the card over gloo) carries every rank's
+    roofline and the stored CPU baseline (bench.py stored_cpu_baseline), labelled as stored."""
+    d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--log-n", "12", "--steps", "2",
+                  "--warmup", "1", "--lanes", "2", "--no-cpu-baseline", timeout=300)
+    check_contract(d, 2, 1, n_gpus=2)
+    cb = d["cpu_baseline"]
+    assert cb["source"].startswith("stored") and cb["value"] > 0 and cb["cores"] == 32
+    pr = d["roofline"]["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1] and all(r["frac"] > 0 for r in pr)
+    assert d["host_cores"]["lanes_run"] == 2
