@@ -100,7 +100,7 @@ def parse():
                     help="concurrent prover lanes per GPU (prove mode): independent contexts "
                          "with their own streams, each driven by a host thread. 0 = 12 at "
                          "n >= 2^18, 14 at 2^15..2^17, 16 below (2 HIP hardware queues per "
-                         "lane; round-3 sweep tools/gpu_r03_lanes.sh in DESIGN §6)")
+                         "lane; round-3 / round-4 lane sweeps in DESIGN §6)")
     ap.add_argument("--fit-lanes", action="store_true",
                     help="prove mode: lower the lanes per GPU (same on every rank) when the "
                          "warmup's synthesis would need > 90 %% of a rank's CPU share")
@@ -1075,7 +1075,7 @@ def main():
     if world_env is not None and args.gpus is not None and args.gpus != int(world_env):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
     if args.lanes <= 0:
-        # round-3 sweep (tools/gpu_r03_lanes.sh): 2^20 30.2 / 30.3 / 30.7 / 31.4 M at 6 / 8 /
+        # round-3 sweep (profiles/r03_lanes20_sweep.txt): 2^20 30.2 / 30.3 / 30.7 / 31.4 M at 6 / 8 /
         # 10 / 12 lanes; 2^16 24.0 / 24.6 / 25.1 / 22.0 M at 10 / 12 / 14 / 16; 2^12 5.4 / 5.9
         # M at 12 / 16
         args.lanes = 12 if args.log_n >= 18 else 14 if args.log_n >= 15 else 16

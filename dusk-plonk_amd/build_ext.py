@@ -45,7 +45,7 @@ def _compile(src: Path, obj: Path, cflags) -> str:
 
 def build(verbose: bool = True, jobs: int | None = None, variant: str = "",
           extra: tuple = (), only: tuple = ()) -> Path:
-    """variant / extra: an experimental build (extra hipcc flags, e.g. -DPLK_ACC_WAVES=3)
+    """variant / extra: an experimental build (extra hipcc flags, e.g. -DPLK_NTT_MINW=4)
     into build-<variant>/ and libplk-<variant>.so, loaded with PLK_LIB=<path>. only: the
     TU stems that take the extra flags (e.g. ("msm_acc",)); the variant links the default
     build's objects for every other TU, so a one-kernel A/B compiles one file.

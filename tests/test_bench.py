@@ -128,7 +128,8 @@ def test_prove_mode_checks_its_proofs():
                   "--no-cpu-baseline")
     assert d["proofs_checked"] == 3
     hc = d["host_cores"]
-    assert hc["lanes_run"] == 3 and hc["needed_per_rank"] > 0 and hc["available_node"] >= 1
+    assert hc["lanes_run"] == 3 and hc["needed_per_rank"] > 0 and hc["available_per_rank"] >= 1
+    assert "oversubscribed" in hc and len(hc["per_host"]) == 1
 
 
 @pytest.mark.gpu
@@ -207,3 +208,32 @@ def test_prove_line_world2_self_describing():
     pr = d["roofline"]["per_rank"]
     assert [r["rank"] for r in pr] == [0, 1] and all(r["frac"] > 0 for r in pr)
     assert d["host_cores"]["lanes_run"] == 2
+
+
+@pytest.mark.gpu
+def test_msm_bucket_parts_line_is_bit_exact():
+    """`--mode msm --bucket-parts 4`: the 2^16 MSM run as 4 bucket-range parts on one GPU (what
+    each of 4 GPUs runs under --shard-msm), folded, checked against the oracle; per-part times."""
+    d = run_bench("--mode", "msm", "--log-n", "16", "--steps", "2", "--warmup", "1",
+                  "--bucket-parts", "4", "--cpu-threads", "4")
+    check_contract(d, 2, 1)
+    assert d["bit_exact_vs_oracle"] is True
+    bp = d["roofline"]["bucket_parts"]
+    assert bp["parts"] == 4 and len(bp["part_ms_mean"]) == 4 and bp["part_ms_max"] > 0
+
+
+@pytest.mark.gpu
+def test_msm_split_over_ranks_lines():
+    """`--mode msm --shard-msm`: ONE MSM per step split over the ranks by bucket range — at
+    world 1 over RCCL (checked against the oracle) and on 2 gloo ranks sharing the card."""
+    d = run_bench("--mode", "msm", "--shard-msm", "--log-n", "16", "--steps", "2", "--warmup",
+                  "1", "--cpu-threads", "4")
+    assert d["bit_exact_vs_oracle"] is True and d["scaling"] == "strong"
+    assert d["config"]["parallelism"] == "msm-split x1 (buckets)"
+    d2 = run_bench("--gpus", "2", "--mode", "msm", "--shard-msm", "--dist-backend", "gloo",
+                   "--log-n", "16", "--steps", "2", "--warmup", "1", timeout=300)
+    assert d2["n_gpus"] == 2 and d2["scaling"] == "strong"
+    assert d2["config"]["parallelism"] == "msm-split x2 (buckets)"
+    assert d2["roofline"]["bucket_parts"]["parts"] == 2
+    # one MSM per step whatever the world: value = n * steps / time
+    assert d2["value"] == pytest.approx(65536 * 2 / (d2["ms_per_step"] * 2e-3), rel=1e-6)

@@ -207,8 +207,7 @@ np.savez(sys.argv[2], **out)
 
 
 def test_opt_in_plans_vs_oracle(tmp_path, oracle):
-    """The opt-in NTT plans (process-wide environment switches, so in a child process): the
-    persistent software-pipelined pass (PLK_NTT_PF, several tiles per workgroup) and radix
+    """The opt-in NTT plan (a process-wide environment switch, so in a child process): radix
     up to 2^10 (PLK_NTT_MAX_LR: 2^18 / 2^20 in two passes, 1-column tiles, > 64 KiB of LDS
     for the pruned first pass) — bit-exact against the oracle like the default plans."""
     import os
@@ -217,7 +216,7 @@ def test_opt_in_plans_vs_oracle(tmp_path, oracle):
     from pathlib import Path
     root = Path(__file__).resolve().parent.parent
     f = tmp_path / "out.npz"
-    env = dict(os.environ, PLK_NTT_PF="16", PLK_NTT_MAX_LR="10")
+    env = dict(os.environ, PLK_NTT_MAX_LR="10")
     subprocess.run([sys.executable, "-c", _OPT_IN_SCRIPT, str(root), str(f)], env=env, check=True,
                    timeout=240)
     d = np.load(f)
