@@ -115,10 +115,12 @@ struct plk_srs {
   size_t n = 0;              // number of SRS points
   uint32_t c = 16;           // window bits
   uint32_t windows = 16;     // ceil(256 / c)
-  // the top window's digits (fewer than c - 1 bits when c does not divide 255) are scaled by
-  // 2^top_shift and its table row pre-divided by it (msm_prepare_srs): the same products,
-  // spread over the whole bucket range instead of piled into its low end (msm.hip digit_at)
-  uint32_t top_shift = 0;
+  // balanced windows (round 5): when c does not divide 255, the top `narrow` windows are
+  // c - 1 bits wide (narrow = c W - 255) and their digits come scaled by 2, their table rows
+  // pre-divided by 2 (msm_prepare_srs, msm.hip digit_at): every window spreads over the whole
+  // bucket range, without the short top window whose few digit values piled extra entries
+  // onto a few hot buckets
+  uint32_t narrow = 0;
   plk::DevBuf points;        // affine, plk::G1Affine (96 B), n entries; inf flags separate
   plk::DevBuf inf;           // uint8 per point
   plk::DevBuf table;         // precomputed 2^(c*w) * P_i, affine, windows * n entries

@@ -48,11 +48,14 @@ namespace {
 constexpr uint32_t kHistThreads = 1024;
 constexpr uint32_t kHistBlocksMax = 256;  // histogram / scatter workgroups per slot
 
-// signed c-bit digit w of canonical scalar s (carry threaded through the caller); the top
-// window's (non-negative, < 2^(c-1 - top_shift)) digit comes scaled by 2^top_shift
+// signed digit w of canonical scalar s (carry threaded through the caller): windows
+// 0 .. W - narrow - 1 take c bits, the top `narrow` ones c - 1 bits (plk_srs::narrow), their
+// digits (|d| <= 2^(c-2)) scaled by 2 so that they span the bucket range too
 __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, const MsmCfg& cfg, uint32_t& carry) {
-  const uint32_t c = cfg.c;
-  const uint32_t o = w * c;
+  const uint32_t wn = cfg.W - cfg.narrow;  // first narrow window
+  const bool nar = w >= wn;
+  const uint32_t c = cfg.c - (nar ? 1u : 0u);
+  const uint32_t o = nar ? wn * cfg.c + (w - wn) * c : w * cfg.c;
   uint32_t val = 0;
   if (o < 256) {
     // words wd, wd + 1 by a 3-level select tree: indexing s.v with a run-time wd put the
@@ -77,7 +80,7 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, const MsmCfg& c
   } else {
     carry = 0;
   }
-  return w + 1 == cfg.W ? d << cfg.top_shift : d;
+  return nar ? d * 2 : d;
 }
 
 __device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t& i1) {
@@ -553,6 +556,9 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
 // per-bucket task counts on the way; (3) the task records, as k_make_tasks does.
 constexpr uint32_t kFineBits = 10;
 constexpr uint32_t kFine = 1u << kFineBits;  // buckets per coarse bin = threads of k_fine
+// A bucket-range part (parts > 1) of 2^(c-1) / parts buckets keeps >= 256 coarse bins (k_fine
+// / k_make_tasks_wide workgroups) with bins of 2^FB buckets, FB = max(8, 10 - log2 parts)
+constexpr uint32_t kFineBitsMin = 8;
 constexpr uint32_t kCoarseMax = 4096;        // coarse bins (B <= 2^22, c <= 23)
 // bucket reduction: runs of K = 2^rb buckets per lane. Batches of several MSMs (the
 // prover's commit groups, with other proofs' kernels beside them) take 16. A lone MSM's
@@ -617,7 +623,7 @@ __device__ __forceinline__ void block_scan_excl(uint32_t (&v)[K], uint32_t (&tot
 
 // Wide pass 1: per-workgroup histogram of the coarse bins (bucket >> kFineBits), written whole
 __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg cfg, uint32_t NC,
-                                                        uint32_t* __restrict__ blockhist) {
+                                                        uint32_t fb, uint32_t* __restrict__ blockhist) {
   __shared__ uint32_t hist[kCoarseMax];
   const uint32_t slot = blockIdx.y;
   uint32_t i0, i1;
@@ -632,7 +638,7 @@ __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg c
     for (uint32_t w = 0; w < cfg.W; ++w) {
       const int d = digit_at(s, w, cfg, carry);
       const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
-      if (b < cfg.B) atomicAdd(&hist[b >> kFineBits], 1u);
+      if (b < cfg.B) atomicAdd(&hist[b >> fb], 1u);
     }
   }
   __syncthreads();
@@ -644,7 +650,7 @@ __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg c
 // bin offsets (workgroup 0 also stores them), then each digit's (code, bucket) takes the next
 // slot of its bin in this workgroup's range.
 __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCfg cfg, uint32_t NC,
-                                                           uint64_t n_srs,
+                                                           uint32_t fb, uint64_t n_srs,
                                                            const uint32_t* __restrict__ ccounts,
                                                            const uint32_t* __restrict__ blockhist,
                                                            uint32_t* __restrict__ coarse_off,
@@ -688,7 +694,7 @@ __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCf
       const int d = digit_at(s, w, cfg, carry);
       const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
       if (b < cfg.B) {
-        const uint32_t pos = atomicAdd(&hist[b >> kFineBits], 1u);
+        const uint32_t pos = atomicAdd(&hist[b >> fb], 1u);
         out[pos] = make_uint2((uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u), b);
       }
     }
@@ -699,7 +705,8 @@ __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCf
 // of the bin's entries by bucket into its own region of `sorted`; bucket offsets (global),
 // per-bucket task and full-task offsets relative to the bin, the bin's totals and the
 // global histogram of tail lengths (for the execution order of the tasks).
-__global__ void __launch_bounds__(kFine) k_fine(uint32_t B, uint32_t NC, uint32_t chunk,
+template <uint32_t FB>
+__global__ void __launch_bounds__(1u << FB) k_fine(uint32_t B, uint32_t NC, uint32_t chunk,
                                                 const uint32_t* __restrict__ coarse_off,
                                                 const uint2* __restrict__ tmp, uint64_t tmp_stride,
                                                 uint32_t* __restrict__ sorted, uint64_t sorted_stride,
@@ -708,6 +715,7 @@ __global__ void __launch_bounds__(kFine) k_fine(uint32_t B, uint32_t NC, uint32_
                                                 uint32_t* __restrict__ full_rel,
                                                 uint32_t* __restrict__ bin_tot,
                                                 uint32_t* __restrict__ len_count) {
+  constexpr uint32_t kFine = 1u << FB;
   __shared__ uint32_t cnt[kFine];
   __shared__ uint32_t s_len[kChunkMax];
   __shared__ uint32_t sh[3 * 32];
@@ -766,7 +774,8 @@ __global__ void __launch_bounds__(kFine) k_fine(uint32_t B, uint32_t NC, uint32_
 
 // Wide pass 4: task records in the layout of k_make_tasks (full tasks first, bucket order;
 // tails grouped by length, longest first). Bin bases are sums of the bin totals below.
-__global__ void __launch_bounds__(kFine) k_make_tasks_wide(uint32_t B, uint32_t NC, uint32_t chunk,
+template <uint32_t FB>
+__global__ void __launch_bounds__(1u << FB) k_make_tasks_wide(uint32_t B, uint32_t NC, uint32_t chunk,
                                                            const uint32_t* __restrict__ offsets,
                                                            const uint32_t* __restrict__ task_rel,
                                                            const uint32_t* __restrict__ full_rel,
@@ -793,7 +802,7 @@ __global__ void __launch_bounds__(kFine) k_make_tasks_wide(uint32_t B, uint32_t 
   }
   block_scan_excl<4>(v, tot, sh);
   const uint32_t task_base = tot[0], full_base = tot[1], task_total = tot[2], full_total = tot[3];
-  const uint32_t b = bin * kFine + tid;
+  const uint32_t b = (bin << FB) + tid;
   const uint32_t* off = offsets + (size_t)slot * (B + 1);
   const uint32_t start = off[b], cnt = off[b + 1] - start;
   const uint32_t t0 = task_base + task_rel[(size_t)slot * B + b];
@@ -1346,12 +1355,15 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   if ((st = ws_reserve(s, w, max_len ? max_len : 1, (uint32_t)count, stream))) return st;
   // B: the buckets this call reduces (all 2^(c-1), or a part's range of them)
   const uint32_t B_all = 1u << (s->c - 1), B = B_all / parts;
-  const MsmCfg cfg{s->c, s->windows, B, s->top_shift, part * B};
+  const MsmCfg cfg{s->c, s->windows, B, s->narrow, part * B};
   // wide bucket sets: two-level sort and run-sum reduction; the bit sums then run over the
   // NR = B / 2^rb runs instead of the buckets
   const bool wide = B_all > kLdsBuckets;
   const uint32_t rb = run_bits(B, (uint32_t)count);
-  const uint32_t NC = B >> kFineBits, NR = B >> rb;
+  // coarse-bin width (wide sets): 2^10 buckets, finer for a part's narrower range
+  uint32_t fb = kFineBits;
+  while (fb > kFineBitsMin && (1u << (kFineBits - fb)) < parts) --fb;
+  const uint32_t NC = B >> fb, NR = B >> rb;
   const uint32_t G = cdiv(wide ? NR : B, 256);  // a power of two
   if (parts > 1 && NR != 256u * G) return PLK_E_DEVICE;  // the part offset's Horner seed below
   const uint32_t nbits = 8 + (uint32_t)__builtin_ctz(G);  // T_0..T_7 of u, one per bit of g
@@ -1392,7 +1404,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   if (wide) {
     if (max_len) {
       hipLaunchKernelGGL(k_chist, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
-                         cfg, NC, w.blockhist.as<uint32_t>());
+                         cfg, NC, fb, w.blockhist.as<uint32_t>());
     } else {
       PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * NC * 4, stream));
     }
@@ -1400,22 +1412,29 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                        w.blockhist.as<uint32_t>(), hist_blocks, NC, w.counts.as<uint32_t>(),
                        w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>());
     hipLaunchKernelGGL(k_cscatter, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
-                       cfg, NC, (uint64_t)s->n, (const uint32_t*)w.counts.as<uint32_t>(),
+                       cfg, NC, fb, (uint64_t)s->n, (const uint32_t*)w.counts.as<uint32_t>(),
                        (const uint32_t*)w.blockhist.as<uint32_t>(), w.coarse_off.as<uint32_t>(),
                        w.tmp.as<uint2>(), (uint64_t)(w.sorted_stride - 1));
-    hipLaunchKernelGGL(k_fine, dim3(NC, slots), dim3(kFine), 0, stream, B, NC, chunk,
-                       (const uint32_t*)w.coarse_off.as<uint32_t>(), (const uint2*)w.tmp.as<uint2>(),
-                       (uint64_t)(w.sorted_stride - 1), w.sorted.as<uint32_t>(),
-                       (uint64_t)w.sorted_stride, w.offsets.as<uint32_t>(),
-                       w.task_rel.as<uint32_t>(), w.full_off.as<uint32_t>(),
-                       w.bin_tot.as<uint32_t>(), w.len_cur.as<uint32_t>());
-    hipLaunchKernelGGL(k_make_tasks_wide, dim3(NC, slots), dim3(kFine), 0, stream, B, NC, chunk,
-                       (const uint32_t*)w.offsets.as<uint32_t>(),
-                       (const uint32_t*)w.task_rel.as<uint32_t>(),
-                       (const uint32_t*)w.full_off.as<uint32_t>(),
-                       (const uint32_t*)w.bin_tot.as<uint32_t>(),
-                       (const uint32_t*)w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>(),
-                       w.task_off.as<uint32_t>(), w.tasks.as<uint2>(), (uint64_t)w.task_stride);
+#define PLK_FINE_LAUNCH(FB)                                                                       \
+  do {                                                                                            \
+    hipLaunchKernelGGL(k_fine<FB>, dim3(NC, slots), dim3(1u << FB), 0, stream, B, NC, chunk,      \
+                       (const uint32_t*)w.coarse_off.as<uint32_t>(), (const uint2*)w.tmp.as<uint2>(), \
+                       (uint64_t)(w.sorted_stride - 1), w.sorted.as<uint32_t>(),                  \
+                       (uint64_t)w.sorted_stride, w.offsets.as<uint32_t>(),                       \
+                       w.task_rel.as<uint32_t>(), w.full_off.as<uint32_t>(),                      \
+                       w.bin_tot.as<uint32_t>(), w.len_cur.as<uint32_t>());                       \
+    hipLaunchKernelGGL(k_make_tasks_wide<FB>, dim3(NC, slots), dim3(1u << FB), 0, stream, B, NC,  \
+                       chunk, (const uint32_t*)w.offsets.as<uint32_t>(),                          \
+                       (const uint32_t*)w.task_rel.as<uint32_t>(),                                \
+                       (const uint32_t*)w.full_off.as<uint32_t>(),                                \
+                       (const uint32_t*)w.bin_tot.as<uint32_t>(),                                 \
+                       (const uint32_t*)w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>(),      \
+                       w.task_off.as<uint32_t>(), w.tasks.as<uint2>(), (uint64_t)w.task_stride);  \
+  } while (0)
+    if (fb == 10) PLK_FINE_LAUNCH(10);
+    else if (fb == 9) PLK_FINE_LAUNCH(9);
+    else PLK_FINE_LAUNCH(8);
+#undef PLK_FINE_LAUNCH
   } else if (sort_one) {
     hipLaunchKernelGGL(k_sort_one, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
                        (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,

@@ -29,7 +29,7 @@ constexpr uint32_t kMaxSlots = 16;  // independent MSMs per batch
 
 struct MsmCfg {
   uint32_t c, W, B;
-  uint32_t top_shift;  // plk_srs::top_shift
+  uint32_t narrow;  // plk_srs::narrow: the top `narrow` windows are c - 1 bits, digits x 2
   // bucket range of a part (msm_run_batch parts > 1: the wide-set sort keeps only digits of
   // buckets [b_lo, b_lo + B), renumbered from 0); b_lo = 0 for a whole MSM
   uint32_t b_lo;

@@ -2,7 +2,7 @@
 //
 // setup(k, rng) (zksnarks, un-vendored; tests/*.rs:24) restated with an
 // explicit secret tau: g1[i] = [tau^i] G1. The MSM (msm.hip) additionally needs
-// table[w][i] = 2^(c*w) * g1[i] in affine form (the top row 2^(c*w - top_shift) g1[i]); both are produced here with XYZZ
+// table[w][i] = 2^(o_w - s_w) * g1[i] in affine form (balanced windows, msm_prepare_srs); both are produced here with XYZZ
 // arithmetic and converted to affine by batch inversion (Montgomery's trick, one Fermat
 // inversion per kBatchAff points).
 #include <hip/hip_runtime.h>
@@ -97,7 +97,8 @@ static uint32_t choose_c(size_t n) {
   // PLK_MSM_C (tests, experiments): a fixed window size for every SRS prepared afterwards
   if (const char* e = getenv("PLK_MSM_C")) {
     const int c = atoi(e);
-    if (c >= 8 && c <= 23) return (uint32_t)c;
+    // the balanced window layout needs (c - 1) ceil(255 / c) <= 255: not c = 21, 23
+    if (c >= 8 && c <= 22 && c != 21) return (uint32_t)c;
   }
   // 2^20 points and up: c = 20, 13 windows (16 at c = 16). Entries N * W fall 19 %; the
   // 2^19 buckets (~26 entries each) go through the wide-set sort and the run-sum
@@ -130,16 +131,15 @@ static uint32_t choose_c(size_t n) {
 int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   s->c = choose_c(s->n);
   s->windows = (255 + s->c - 1) / s->c;  // scalars recoded from [0, (r-1)/2] (< 2^254)
-  // the top window holds bits c (W - 1) .. 253: with the carry its digit is at most
-  // 2^(254 - c (W - 1)); below 2^(c - 1) it is scaled up to span the buckets (plk_srs::top_shift;
-  // c = 20: digits <= 2^14 would pile 2^20 extra entries onto the lowest 2^14 of 2^19 buckets,
-  // doubling the run-sum chains there). PLK_TOP_SPREAD=0: off (experiments)
-  {
-    const int tb = 254 - (int)(s->c * (s->windows - 1));
-    const char* e = getenv("PLK_TOP_SPREAD");
-    const bool on = !e || atoi(e) != 0;
-    s->top_shift = on && tb >= 0 && tb < (int)s->c - 1 ? (uint32_t)((int)s->c - 1 - tb) : 0u;
-  }
+  // balanced windows (round 5): the W windows cover exactly 255 bits, the top `narrow` = c W -
+  // 255 of them c - 1 bits wide with digits scaled by 2 (msm.hip digit_at) and table rows
+  // pre-divided by 2, so every window spreads over all 2^(c-1) buckets: even buckets hold the
+  // wide windows' entries, odd ones also the narrow windows' (c = 20: 8 x 20 + 5 x 19 bits,
+  // 16 / 36 entries per 2^20 scalars, every run of >= 2 buckets the same load). Round 4's
+  // short top window (c = 20: 14 bits, digits x 32) piled 2^20 entries onto 2^14 buckets,
+  // 88 entries against 24: chains in the reduction of a part of a split MSM and in the narrow
+  // path's bucket sums (c = 10: 16 buckets at 2.3x)
+  s->narrow = s->c * s->windows - 255;
   const size_t n = s->n;
   int st;
   if ((st = s->table.alloc((size_t)s->windows * n * sizeof(G1Affine)))) return st;
@@ -152,10 +152,12 @@ int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   if ((st = pref.alloc(n * sizeof(Fp)))) return st;
   G1Affine* tab = s->table.as<G1Affine>();
   uint8_t* tinf = s->table_inf.as<uint8_t>();
+  // row w = 2^(o_w - s_w) P (o_w the window's bit offset, s_w = 1 for narrow windows): from
+  // row w - 1 by c doublings while both are wide, c - 1 from the first narrow one on
   for (uint32_t w = 1; w < s->windows; ++w) {
     hipLaunchKernelGGL(k_double_c, dim3(cdiv(n, 256)), dim3(256), 0, stream, tab + (w - 1) * n,
                        tinf + (w - 1) * n, (uint64_t)n,
-                       w + 1 == s->windows ? s->c - s->top_shift : s->c, temp.as<G1xyzz>());
+                       w < s->windows - s->narrow ? s->c : s->c - 1, temp.as<G1xyzz>());
     hipLaunchKernelGGL(k_batch_affine, dim3(cdiv(cdiv(n, kBatchAff), 128)), dim3(128), 0, stream,
                        temp.as<G1xyzz>(), (uint64_t)n, pref.as<Fp>(), tab + w * n, tinf + w * n);
     PLK_HIP_TRY(hipGetLastError());

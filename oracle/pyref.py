@@ -415,38 +415,54 @@ def srs_setup(tau: int, count: int):
     return out
 
 
+def msm_window_layout(c: int):
+    """The MSM's window layout (srs.hip msm_prepare_srs, round 5 "balanced windows"): W =
+    ceil(255 / c) windows covering exactly 255 bits, the top `narrow` = c W - 255 of them
+    c - 1 bits wide with their digits scaled by 2 (table rows pre-divided by 2). Returns
+    [(bit offset, width, scale shift)] per window."""
+    W = (FR_BITS + c - 1) // c
+    narrow = c * W - FR_BITS
+    out, o = [], 0
+    for w in range(W):
+        nar = w >= W - narrow
+        cw = c - 1 if nar else c
+        out.append((o, cw, 1 if nar else 0))
+        o += cw
+    assert o == FR_BITS
+    return out
+
+
 def msm_bucket_part(points, scalars, c: int, part: int, parts: int):
     """The share of bucket range `part` of `parts` of a signed-digit Pippenger MSM with window
     c (plk_commit_batch_dev_part's definition; a checker for the split, not the reference's
     algorithm): sum over the entries whose bucket |d| - 1 lies in [part, part + 1) x
-    2^(c-1) / parts of d * 2^(c w) * P_i, with the scalar first brought to [0, (r-1)/2] (s or
-    r - s with the digits' signs flipped), W = ceil(255 / c) signed windows (|d| <= 2^(c-1))
-    and the short top window's digits scaled by 2^top_shift into the bucket range (their
-    table row divided by the same: srs.hip top_shift). The shares of all parts sum to
-    sum_i s_i P_i. Each entry's contribution is a multiple of its point, so the share is a
-    plain MSM with per-point sums of those multiples (affine result, None = identity)."""
-    W = (FR_BITS + c - 1) // c
-    tb = 254 - c * (W - 1)
-    ts = c - 1 - tb if 0 <= tb < c - 1 else 0
+    2^(c-1) / parts of d * 2^(offset) * P_i, with the scalar first brought to [0, (r-1)/2] (s or
+    r - s with the digits' signs flipped) and the windows of msm_window_layout (narrow windows'
+    digits scaled by 2 into the bucket range, their table rows divided by 2). The shares of all
+    parts sum to sum_i s_i P_i. Each entry's contribution is a multiple of its point, so the
+    share is a plain MSM with per-point sums of those multiples (affine result, None =
+    identity)."""
+    layout = msm_window_layout(c)
     B = 1 << (c - 1)
     lo, hi = part * B // parts, (part + 1) * B // parts
-    inv_ts = pow(1 << ts, -1, R_MOD)
+    inv2 = pow(2, -1, R_MOD)
     per_point = []
     for s in scalars:
         s %= R_MOD
         neg = s > (R_MOD - 1) // 2
         h = R_MOD - s if neg else s
         acc, carry = 0, 0
-        for w in range(W):
-            val = (h >> (w * c)) & ((1 << c) - 1) if w * c < 256 else 0
+        for o, cw, sh in layout:
+            val = (h >> o) & ((1 << cw) - 1)
             d = val + carry
-            carry = 1 if d > B else 0
-            d -= (1 << c) if carry else 0
-            mult = pow(2, c * w, R_MOD)
-            if w == W - 1:
-                d <<= ts
-                mult = mult * inv_ts % R_MOD
+            carry = 1 if d > (1 << (cw - 1)) else 0
+            d -= (1 << cw) if carry else 0
+            mult = pow(2, o, R_MOD)
+            if sh:
+                d *= 2
+                mult = mult * inv2 % R_MOD
             if d and lo <= abs(d) - 1 < hi:
                 acc += (-d if neg else d) * mult
+        assert carry == 0
         per_point.append(acc % R_MOD)
     return msm_naive(points, per_point)

@@ -116,35 +116,40 @@ def test_bucket_parts_identity(c, parts):
     unsigned < B/parts, digit 0 wrapping out of range), reduces them as a wide set of B/parts
     buckets and adds b_lo sum_b S_b on the host; the parts' shares sum to sum_b (b+1) S_b.
     Integers mod r stand in for the points (the identities are linear): the whole MSM
-    sum_i s_i P_i with the signed recoding, the scalar halving and the spread top window."""
+    sum_i s_i P_i with the signed recoding, the scalar halving and the balanced windows
+    (srs.hip msm_prepare_srs: the top c W - 255 windows c - 1 bits wide, digits x 2)."""
     rng = random.Random(c * 100 + parts)
     W = (255 + c - 1) // c
-    tb = 254 - c * (W - 1)
-    ts = c - 1 - tb if 0 <= tb < c - 1 else 0
+    narrow = c * W - 255  # balanced windows: the top `narrow` are c - 1 bits, digits x 2
     r_mod = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
     q = r_mod  # the group order: r P = 0 is what makes the scalar halving exact
     n = 40
     P = [rng.randrange(q) for _ in range(n)]
     sc = [rng.randrange(r_mod) for _ in range(n - 4)] + [0, 1, r_mod - 1, (r_mod - 1) // 2 + 1]
     B = 1 << (c - 1)
-    inv2ts = pow(1 << ts, -1, q)
+    inv2 = pow(2, -1, q)
     entries = {}  # bucket -> sum of signed table values
     for s, p in zip(sc, P):
         neg = s > (r_mod - 1) // 2
         h = r_mod - s if neg else s
-        d, carry = digits(h, c, W)
-        assert carry == 0
-        for w, x in enumerate(d):
-            if w == W - 1:
-                x <<= ts  # digit_at scales the top window's digit, its table row is pre-divided
-                tv = pow(2, c * w, q) * inv2ts % q * p % q
-            else:
-                tv = pow(2, c * w, q) * p % q
-            if x == 0:
+        o, carry = 0, 0
+        for w in range(W):
+            nar = w >= W - narrow
+            cw = c - 1 if nar else c
+            d = ((h >> o) & ((1 << cw) - 1)) + carry
+            carry = 1 if d > 1 << (cw - 1) else 0
+            d -= (1 << cw) if carry else 0
+            tv = pow(2, o, q) * p % q
+            if nar:  # digit_at scales a narrow window's digit by 2, its table row is halved
+                d *= 2
+                tv = tv * inv2 % q
+            o += cw
+            if d == 0:
                 continue
-            assert abs(x) <= B
-            sign = (x < 0) != neg
-            entries[abs(x) - 1] = (entries.get(abs(x) - 1, 0) + (-tv if sign else tv)) % q
+            assert abs(d) <= B
+            sign = (d < 0) != neg
+            entries[abs(d) - 1] = (entries.get(abs(d) - 1, 0) + (-tv if sign else tv)) % q
+        assert o == 255 and carry == 0
     want = sum(s * p for s, p in zip(sc, P)) % q
     Bp = B // parts
     total = 0
@@ -159,3 +164,47 @@ def test_bucket_parts_identity(c, parts):
         assert local == sum((b + 1) * v for b, v in enumerate(S))
         total += local + b_lo * ssum
     assert total % q == want
+
+
+@pytest.mark.parametrize("c", [8, 10, 13, 15, 16, 17, 18, 19, 20, 22])
+def test_balanced_windows_recoding_and_load(c):
+    """srs.hip's balanced windows: the signed digits of the layout (oracle/pyref.py
+    msm_window_layout) reconstruct every scalar < 2^254 with no final carry, stay within the
+    bucket range after the narrow windows' x 2, and — the point of the layout — every run of
+    two buckets receives the same expected number of entries (no hot buckets)."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "oracle"))
+    import pyref as P
+    layout = P.msm_window_layout(c)
+    B = 1 << (c - 1)
+    rng = random.Random(c)
+    load = [0] * B
+    for s in [0, 1, (1 << 254) - 1] + [rng.randrange(1 << 254) for _ in range(300)]:
+        carry, back = 0, 0
+        for o, cw, sh in layout:
+            d = ((s >> o) & ((1 << cw) - 1)) + carry
+            carry = 1 if d > 1 << (cw - 1) else 0
+            d -= (1 << cw) if carry else 0
+            back += d << o
+            b = abs(d << sh) - 1
+            assert -1 <= b < B
+            if b >= 0:
+                load[b] += 1
+        assert carry == 0 and back == s
+    # expected entries per bucket: a wide window's |d| is uniform on [1, 2^(c-1)], a narrow
+    # one's doubled digit lands on odd-indexed buckets only (b = 2|d| - 1): runs of 2 even out
+    exp = [0.0] * B
+    for o, cw, sh in layout:
+        for b in range(B):
+            exp[b] += (1.0 / B) if not sh else (2.0 / B if b % 2 == 1 else 0.0)
+    runs = [exp[2 * r] + exp[2 * r + 1] for r in range(B // 2)]
+    assert max(runs) - min(runs) < 1e-9
+
+
+def test_balanced_windows_exist_only_for_supported_c():
+    """c W - 255 narrow windows need (c - 1) W <= 255: true for every c srs.hip accepts
+    (8 .. 20 and 22; choose_c refuses PLK_MSM_C = 21 / 23)."""
+    for c in range(8, 24):
+        W = (255 + c - 1) // c
+        assert ((c - 1) * W <= 255) == (c not in (21, 23)), c
