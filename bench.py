@@ -776,8 +776,11 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
             "prove_latency": 1e3 * sum(sum(ln.prove_s) for ln in lanes) / (steps * L),
         },
         "proofs_checked": checked - len(mismatched),
-        "proofs_check": ("each lane's last timed proof re-proved alone on one lane after the "
-                         "timed region, byte-identical"),
+        "proofs_check": ("GPU against GPU: each lane's last timed proof re-proved alone on one "
+                         "lane after the timed region, byte-identical (catches races between "
+                         "concurrent lanes). The oracle check of this configuration (12 lanes "
+                         "at 2^20 against the committed C-oracle proof) is the -m gpu test "
+                         "tests/test_prover_lanes.py::test_twelve_lanes_2_20_concurrent_byte_exact"),
         "host_cores": {**hc, "lanes_requested": len(lanes_all), "lanes_run": L,
                        "note": "lanes x measured synthesis s / step s (warmup) per rank, against "
                                "that rank's own CPU share (cpu_share); ratio = the largest "

@@ -130,6 +130,8 @@ static uint32_t choose_c(size_t n) {
 
 int msm_prepare_srs(plk_srs* s, hipStream_t stream) {
   s->c = choose_c(s->n);
+  // every window would be c - 1 bits (c = 18: 15 x 17 = 255): that is the c - 1 layout
+  if ((s->c - 1) * ((255 + s->c - 1) / s->c) == 255) s->c -= 1;
   s->windows = (255 + s->c - 1) / s->c;  // scalars recoded from [0, (r-1)/2] (< 2^254)
   // balanced windows (round 5): the W windows cover exactly 255 bits, the top `narrow` = c W -
   // 255 of them c - 1 bits wide with digits scaled by 2 (msm.hip digit_at) and table rows

@@ -415,11 +415,18 @@ def srs_setup(tau: int, count: int):
     return out
 
 
+def msm_effective_c(c: int) -> int:
+    """srs.hip msm_prepare_srs: a c whose every window would be c - 1 bits wide (c = 18:
+    15 x 17 = 255) runs as c - 1."""
+    return c - 1 if (c - 1) * ((FR_BITS + c - 1) // c) == FR_BITS else c
+
+
 def msm_window_layout(c: int):
     """The MSM's window layout (srs.hip msm_prepare_srs, round 5 "balanced windows"): W =
     ceil(255 / c) windows covering exactly 255 bits, the top `narrow` = c W - 255 of them
     c - 1 bits wide with their digits scaled by 2 (table rows pre-divided by 2). Returns
     [(bit offset, width, scale shift)] per window."""
+    c = msm_effective_c(c)
     W = (FR_BITS + c - 1) // c
     narrow = c * W - FR_BITS
     out, o = [], 0
@@ -443,7 +450,7 @@ def msm_bucket_part(points, scalars, c: int, part: int, parts: int):
     share is a plain MSM with per-point sums of those multiples (affine result, None =
     identity)."""
     layout = msm_window_layout(c)
-    B = 1 << (c - 1)
+    B = 1 << (msm_effective_c(c) - 1)
     lo, hi = part * B // parts, (part + 1) * B // parts
     inv2 = pow(2, -1, R_MOD)
     per_point = []

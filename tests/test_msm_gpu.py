@@ -198,7 +198,7 @@ def test_commit_batch_dev(plk, gpu_ctx, oracle):
         assert np.array_equal(out[i].words, oracle.msm(pts[:64], p)), i
 
 
-@pytest.mark.parametrize("c,logn", [(17, 10), (20, 12), (18, 14), (20, 16)])
+@pytest.mark.parametrize("c,logn", [(17, 10), (20, 12), (18, 14), (19, 14), (20, 16)])
 def test_msm_wide_buckets_vs_oracle(plk, gpu_ctx, oracle, monkeypatch, c, logn):
     """Wide bucket sets (2^(c-1) > 32 K buckets: the two-level radix sort, the per-bin
     counting sort and the run-sum bucket reduction of msm.hip) at small sizes, forced with

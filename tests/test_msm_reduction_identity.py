@@ -177,7 +177,7 @@ def test_balanced_windows_recoding_and_load(c):
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "oracle"))
     import pyref as P
     layout = P.msm_window_layout(c)
-    B = 1 << (c - 1)
+    B = 1 << (P.msm_effective_c(c) - 1)
     rng = random.Random(c)
     load = [0] * B
     for s in [0, 1, (1 << 254) - 1] + [rng.randrange(1 << 254) for _ in range(300)]:
