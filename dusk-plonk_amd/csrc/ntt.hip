@@ -65,8 +65,12 @@ constexpr uint32_t kDSSmall = 256;
 // passes in the input loop (round 3, slower), the persistent software-pipelined pass with
 // register prefetch (round 3, slower at 2 and 3 waves per SIMD), the last two steps' quad
 // exchange through LDS (round 4, between the barrier form and the DPP form kept below), the
-// radix-4 products one by one (round 4, slower than the pairs kept below) and the
-// constant-twiddle Shoup product (round 4, slower).
+// radix-4 products one by one (round 4, slower than the pairs kept below), the
+// constant-twiddle Shoup product (round 4, slower) and (round 5, commit 3b467e3) a persistent
+// pass for lone transforms whose next tile arrives by LDS-DMA into a staging buffer while the
+// current one computes (static LDS arrays so that only the staging reads wait for the DMA, raw
+// barriers): 75 KiB LDS and 240 VGPRs, 2 workgroups per CU against 4 — dft + idft 2^20 0.309-
+// 0.312 against 0.297 ms, 2^23 2.33-2.36 against 2.07 ms (profiles/r05_ntt_pipe_ab.jsonl).
 // k_ntt_pass minimum waves per SIMD (-DPLK_NTT_MINW=4 caps it at 128 VGPRs)
 #ifndef PLK_NTT_MINW
 #define PLK_NTT_MINW 1
@@ -506,173 +510,6 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
   }
 }
 
-// ---- pipelined pass for a lone transform (round 5, LDS-DMA) ------------------------------
-// A lone transform's tiles fill the chip's workgroup slots exactly once (2^20: 1 024 tiles of
-// 40 KiB, 4 per CU), so every workgroup loads, computes and stores in lockstep: load and store
-// phases no other work overlaps (≈ 28 % of a lone 2^20 transform). Here a
-// persistent workgroup takes tiles blockIdx.x, + gridDim.x, ... and the NEXT tile's packed
-// 32-byte inputs arrive in an LDS staging buffer by global_load_lds_dwordx4 (no VGPR
-// destination) while the current tile's butterflies and stores run; its inter-pass twiddles
-// (or coset factors) are prefetched into registers beside them. The staging buffer and the
-// data planes are separate static LDS arrays, so the compiler's LDS-DMA alias tracking waits
-// (vmcnt) only before the staging reads, and every barrier is a raw s_barrier after
-// lgkmcnt(0) (__syncthreads' fence would wait vmcnt(0) and drain the DMA in flight).
-// LDS: 36 KiB planes + 32 KiB staging + twiddles ≈ 70 KiB: 2 workgroups (2 waves per SIMD)
-// per CU, against 4 for k_ntt_pass. Non-pruned passes of E = 1024 elements, 256 threads.
-typedef __attribute__((address_space(3))) void lds_void;
-constexpr uint32_t kPipeE = 1024, kPipeThreads = 256, kPipeIt = kPipeE / kPipeThreads;
-
-__device__ __forceinline__ void pipe_barrier() {
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) (vmcnt, expcnt untouched)
-  __builtin_amdgcn_s_barrier();
-}
-
-template <int PRE, int POST>
-__global__ void __launch_bounds__(kPipeThreads) k_ntt_pipe(const Fr* __restrict__ in, Fr* __restrict__ out,
-                                                          const Fr* __restrict__ tw,
-                                                          const Fr* __restrict__ ptw,
-                                                          const Fr* __restrict__ pre,
-                                                          const Fr* __restrict__ post, Fr post_scalar,
-                                                          uint32_t log_n, uint32_t lp, uint32_t lr,
-                                                          uint32_t lt, uint64_t len_in) {
-  constexpr uint32_t DS = kDS;
-  __shared__ uint32_t data[kL * DS];                 // limb planes of the current tile
-  __shared__ uint4 stage[2 * kPipeE];                // the next tile, packed: [c][half][tid]
-  __shared__ uint32_t twl_s[kL * (kPipeE / 8)];      // TS = R/2 <= E/8 (lt >= 2)
-  __shared__ uint32_t ztab[kQMax * kL];
-  const uint32_t R = 1u << lr, T = 1u << lt, p = 1u << lp, H = R >> 1, TS = H;
-  uint32_t* twl = twl_s;
-  const uint32_t tid = threadIdx.x, bd = kPipeThreads;
-  const uint32_t nr_log = log_n - lr;
-  const uint32_t nblk = 1u << (log_n - lr - lt);
-  for (uint32_t x = tid; x < TS; x += bd) lds_st(twl, TS, x, ld_rfr(&tw[(size_t)x << nr_log]));
-  for (uint32_t x = tid; x < kQMax * kL; x += bd) ztab[x] = kZTab.v[x];
-  const bool has_aux = PRE == 1 || lp != 0;
-  Fr aux[kPipeIt];
-  // the DMA of tile `tile`'s inputs (element e = tid + c bd: row e >> lt, column e & (T - 1);
-  // clamped for zero-padded inputs, the padding is a select at the unpack) and its aux loads
-  auto prefetch = [&](uint32_t tile) {
-    const uint32_t i0 = tile << lt;
-#pragma unroll
-    for (uint32_t c = 0; c < kPipeIt; ++c) {
-      const uint32_t e = tid + c * bd;
-      const size_t g = (size_t)(i0 + (e & (T - 1))) + ((size_t)(e >> lt) << nr_log);
-      const size_t gc = g < len_in ? g : 0;
-      const uint4* src = reinterpret_cast<const uint4*>(&in[gc]);
-      const uint32_t wbase = (tid & ~63u) + (2 * c) * bd;  // wave-uniform LDS base, half 0
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)&stage[wbase], 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(src + 1), (lds_void*)&stage[wbase + bd], 16, 0, 0);
-      if (PRE == 1) aux[c] = ld_fr(&pre[gc]);
-      else if (lp != 0) aux[c] = ld_fr(&ptw[((size_t)(e >> lt) << lp) + ((i0 + (e & (T - 1))) & (p - 1))]);
-    }
-  };
-  uint32_t tile = blockIdx.x;
-  prefetch(tile);
-  pipe_barrier();  // twl / ztab staged
-  const bool r2first = (lr & 1) && lr >= 3;
-  for (;;) {
-    const uint32_t i0 = tile << lt;
-    // this thread's staged elements (written by its own lane's DMA: no barrier needed, the
-    // compiler waits vmcnt before these reads)
-    RFr v[kPipeIt];
-#pragma unroll
-    for (uint32_t c = 0; c < kPipeIt; ++c) {
-      const uint4 a = stage[(2 * c) * bd + tid], b = stage[(2 * c + 1) * bd + tid];
-      Fr x;
-      x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
-      x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
-      const uint32_t e = tid + c * bd;
-      const size_t g = (size_t)(i0 + (e & (T - 1))) + ((size_t)(e >> lt) << nr_log);
-      RFr y = g < len_in ? rx_unpack(x) : rx_zero<FrCfg>();
-      if (has_aux) y = rx_mul(y, rx_unpack(aux[c]));
-      v[c] = y;
-    }
-    // the staging reads have returned: the next tile's DMA may overwrite the buffer
-    const uint32_t next = tile + gridDim.x;
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    if (next < nblk) prefetch(next);
-    int lh = (int)lr - 1;
-    if (r2first) {  // the stage of half R/2 on the registers (rows j, j + R/2 of one column)
-#pragma unroll
-      for (uint32_t c = 0; c < kPipeIt / 2; ++c) {
-        const uint32_t e = tid + c * bd;
-        const RFr a = v[c], u = v[c + kPipeIt / 2];
-        lds_std<DS>(data, e, reduce_q(add_u(a, u), ztab));
-        lds_std<DS>(data, e + kPipeE / 2, twmul(sub_u(a, u), twl, TS, e >> lt));
-      }
-      lh -= 1;
-    } else {
-#pragma unroll
-      for (uint32_t c = 0; c < kPipeIt; ++c) lds_std<DS>(data, tid + c * bd, v[c]);
-    }
-    pipe_barrier();
-    for (; lh >= 1; lh -= 2) {
-      const uint32_t h = 1u << (lh - 1);
-      const uint32_t sh1 = lr - 1 - lh, sh2 = lr - lh;
-      if (lh == 3 && lr >= 5) {  // halves 8, 4, quad transpose in registers, halves 2, 1
-        for (uint32_t g = tid; g < (kPipeE >> 2); g += bd) {
-          const uint32_t r = g & 3u, t = (g >> 2) & (T - 1), B = g >> (2 + lt);
-          const uint32_t j = (B << 4) + r;
-          RFr x0 = lds_ldd<DS>(data, (j << lt) + t), x1 = lds_ldd<DS>(data, ((j + 4) << lt) + t);
-          RFr x2 = lds_ldd<DS>(data, ((j + 8) << lt) + t), x3 = lds_ldd<DS>(data, ((j + 12) << lt) + t);
-          RFr o0, o1, o2, o3;
-          r4_math(twl, TS, ztab, r, 4, lr - 4, lr - 3, x0, x1, x2, x3, o0, o1, o2, o3);
-          quad_transpose(o0, o1, o2, o3);
-          const uint32_t jq = (B << 4) + (r << 2);
-          r4_step<DS>(data, twl, TS, ztab, 0, 1, lr - 2, lr - 1, (jq << lt) + t, ((jq + 1) << lt) + t,
-                      ((jq + 2) << lt) + t, ((jq + 3) << lt) + t, o0, o1, o2, o3);
-        }
-        lh -= 2;
-        pipe_barrier();
-        continue;
-      }
-      for (uint32_t g = tid; g < (kPipeE >> 2); g += bd) {
-        const uint32_t t = g & (T - 1), jg = g >> lt;
-        const uint32_t r = jg & (h - 1);
-        const uint32_t j = ((jg >> (lh - 1)) << (lh + 1)) + r;
-        const uint32_t a0 = (j << lt) + t, a1 = ((j + h) << lt) + t;
-        const uint32_t a2 = ((j + 2 * h) << lt) + t, a3 = ((j + 3 * h) << lt) + t;
-        const RFr x0 = lds_ldd<DS>(data, a0), x1 = lds_ldd<DS>(data, a1);
-        const RFr x2 = lds_ldd<DS>(data, a2), x3 = lds_ldd<DS>(data, a3);
-        r4_step<DS>(data, twl, TS, ztab, r, h, sh1, sh2, a0, a1, a2, a3, x0, x1, x2, x3);
-      }
-      pipe_barrier();
-    }
-    if (lh == 0) {  // odd radix without r2first: last stage of half 1
-      for (uint32_t b = tid; b < (kPipeE >> 1); b += bd) {
-        const uint32_t t = b & (T - 1), j1 = (b >> lt) << 1;
-        const RFr a = lds_ldd<DS>(data, (j1 << lt) + t);
-        const RFr c = lds_ldd<DS>(data, ((j1 + 1) << lt) + t);
-        lds_std<DS>(data, (j1 << lt) + t, reduce_q(add_u(a, c), ztab));
-        lds_std<DS>(data, ((j1 + 1) << lt) + t, reduce_q(rx_sub_u<FrCfg, 6>(a, c), ztab));
-      }
-      pipe_barrier();
-    }
-    for (uint32_t o = tid; o < kPipeE; o += bd) {
-      uint32_t t, m;
-      if (p >= T) {
-        t = o & (T - 1);
-        m = o >> lt;
-      } else {
-        const uint32_t s = o & (p - 1);
-        m = (o >> lp) & (R - 1);
-        t = ((o >> (lp + lr)) << lp) + s;
-      }
-      const uint32_t i = i0 + t;
-      const uint32_t k = i & (p - 1);
-      const size_t pos = ((size_t)(i - k) << lr) + k + ((size_t)m << lp);
-      RFr val = lds_ldd<DS>(data, (bitrev(m, lr) << lt) + t);
-      if (POST == 1) val = rx_mul(val, rx_unpack(post_scalar));
-      else if (POST == 2) val = rx_mul(val, ld_rfr(&post[pos]));
-      else val = reduce_q(val, ztab);
-      st_fr(&out[pos], rx_pack_canonical(val));
-    }
-    if (next >= nblk) break;
-    tile = next;
-    pipe_barrier();  // this tile's output reads before the next tile's plane stores
-  }
-}
-
 // pass twiddles: out[(j << lp) + k] = w_N^{(j k) << shift} for j < R, k < p (R' domain;
 // tw is the R'-domain power table of the same direction)
 __global__ void k_pass_twiddles(const Fr* __restrict__ tw, Fr* __restrict__ out, uint32_t lp,
@@ -896,15 +733,6 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     const size_t lds = ((size_t)(small ? kDSSmall : kDS) + ((1u << ps.lr) >> (prune ? 0 : 1)) + kQMax) *
                        kL * sizeof(uint32_t);
     dim3 grid(blocks, count);
-    // a lone transform's unpruned 1 024-element passes: the pipelined persistent pass
-    // (k_ntt_pipe) on 2 workgroups per CU; PLK_NTT_PIPE=0 keeps k_ntt_pass (A/B)
-    static const bool pipe_on = [] {
-      const char* e = getenv("PLK_NTT_PIPE");
-      return !e || atoi(e) != 0;
-    }();
-    const uint32_t pipe_grid = 2u * (uint32_t)d->ctx->cus;
-    const bool pipe = pipe_on && count == 1 && !prune && !small && E == kPipeE && bd == kPipeThreads &&
-                      ps.lt >= 2 && bt.group == 0 && blocks >= 2 * pipe_grid;
     const Fr* ptw = q == 0 ? nullptr
                            : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
     NttStrides str;
@@ -930,19 +758,7 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     if (small) PLK_LAUNCH_DS(PRE, POST, PRUNE, kDSSmall);          \
     else PLK_LAUNCH_DS(PRE, POST, PRUNE, kDS);                     \
   } while (0)
-#define PLK_PIPE(PRE, POST)                                                                    \
-  hipLaunchKernelGGL((k_ntt_pipe<PRE, POST>), dim3(pipe_grid), dim3(kPipeThreads), 0, stream, src,   \
-                     dst, tw, ptw, pre_table ? pre_table : d->coset_pow.as<Fr>(),                 \
-                     bt.post ? bt.post : d->icoset_scale.as<Fr>(), n_inv_rx, d->log_n, ps.lp,     \
-                     ps.lr, ps.lt, lin)
-    if (pipe) {
-      if (pre == 0 && post == 0) PLK_PIPE(0, 0);
-      else if (pre == 1 && post == 0) PLK_PIPE(1, 0);
-      else if (pre == 0 && post == 1) PLK_PIPE(0, 1);
-      else if (pre == 0 && post == 2) PLK_PIPE(0, 2);
-      else if (pre == 1 && post == 1) PLK_PIPE(1, 1);
-      else PLK_PIPE(1, 2);
-    } else if (prune) {
+    if (prune) {
       if (pre == 1) PLK_LAUNCH(1, 0, 1);
       else PLK_LAUNCH(0, 0, 1);
     } else if (pre == 0 && post == 0) PLK_LAUNCH(0, 0, 0);
@@ -953,7 +769,6 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     else PLK_LAUNCH(1, 2, 0);
 #undef PLK_LAUNCH_DS
 #undef PLK_LAUNCH
-#undef PLK_PIPE
     PLK_HIP_TRY(hipGetLastError());
     src = dst;
   }
