@@ -180,21 +180,12 @@ static_assert(RxMultiple<FpCfg>{rx_multiple<FpCfg>(12, false)}.v[RxShape<FpCfg>:
 
 #define PLK_RX __device__ __forceinline__
 
-#ifndef PLK_RX_PIN
-#define PLK_RX_PIN 0
-#endif
-// acc += x * y as ONE v_mad_u64_u32 on the running column accumulator. With PLK_RX_PIN
-// (experiment, off) each step is followed by a use-only empty asm, so LLVM's reassociation
-// cannot split a column (it otherwise sums a column's products into a fresh accumulator and
-// adds the carried one with a 64-bit v_lshl_add_u64 per column): 4 401 instead of 4 579
-// instructions per mixed addition, but one dependent chain per product measured 3-4 %
-// SLOWER (6.02-6.14e9 against 6.28-6.35e9 additions/s, profiles/r04_ubench_acc_pins.txt).
-PLK_RX void rx_madd(uint64_t& acc, uint32_t x, uint32_t y) {
-  acc += (uint64_t)x * y;
-#if PLK_RX_PIN
-  __asm__ volatile("" ::"v"(acc));
-#endif
-}
+// acc += x * y as ONE v_mad_u64_u32 on the running column accumulator. (Round 4 measured a
+// use-only empty asm after each step, which keeps LLVM from splitting a column: 4 401 instead
+// of 4 579 instructions per mixed addition, but one dependent chain per product ran 3-4 %
+// SLOWER, profiles/r04_ubench_acc_pins.txt; removed in round 5. The product groups below pin
+// with "+v" instead.)
+PLK_RX void rx_madd(uint64_t& acc, uint32_t x, uint32_t y) { acc += (uint64_t)x * y; }
 
 // Close column k of a split-capable product: acc holds the products (+ the incoming
 // carry), s2 the reduction terms and s3 a second product set (split columns only; both 0

@@ -153,9 +153,11 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
 //                                                   r04_tail_modes_small_ab.jsonl)
 //   2^16  26.2-26.9 / 24.1-26.2 / -3 % vs 0   -> 0
 //   2^20  32.5-32.7 / 32.1-32.3 / +0.6 % vs 0 -> 2
-// 2^15, 2^17 and 2^18 follow their neighbours' row (0: both neighbours of 2^17 / 2^18 prefer
-// the single-lane trees or gain < 1 % from quads, and 2^15 sits between 2^14's tie and
-// 2^16's 0); 2^19 and up as 2^20.
+// and, round 5 (profiles/r05_small_and_tail_policy_ab.jsonl, two interleaved runs each):
+//   2^15  21.2-21.4 / 20.3-20.9 / 21.3-21.5   -> 0 (2 within noise)
+//   2^17  29.1-29.2 / 28.5-28.5 / 29.0-29.2   -> 0
+//   2^18  29.6-29.8 / 29.0-29.2 / 29.5-29.6   -> 0
+// 2^19 and up as 2^20.
 inline int lane_tail_policy(uint64_t n) {
   if (n <= (1ull << 13)) return 1;
   if (n == (1ull << 14)) return 2;
