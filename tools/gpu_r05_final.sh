@@ -28,6 +28,9 @@ for k in 12 14 16 18 20; do
   timeout -k 10 400 python bench.py --log-n $k --steps 10 --warmup 3 --no-cpu-baseline >> $O/sizes.jsonl 2>> $O/sizes.err || exit 1
 done
 timeout -k 10 300 python bench.py --mode msm --log-n 20 --steps 20 --warmup 3 --no-cpu-baseline --bucket-parts 8 > $O/parts8.json || exit 1
+for L in 10 14 16; do
+  timeout -k 10 300 python bench.py --lanes $L --steps 8 --warmup 3 --no-cpu-baseline >> $O/lanes20.jsonl 2>> $O/lanes20.err || exit 1
+done
 python3 -c "
 import json
 for f in ['bench_default', 'ntt', 'msm', 'parts8']:
@@ -35,4 +38,6 @@ for f in ['bench_default', 'ntt', 'msm', 'parts8']:
     print(f, round(d['value'] / 1e6, 2), round(d['ms_per_step'], 3), round(r['frac'], 3))
 for l in open('$O/sizes.jsonl'):
     d = json.loads(l); print(d['config']['log_n'], round(d['value'] / 1e6, 2))
+for l in open('$O/lanes20.jsonl'):
+    d = json.loads(l); print('lanes', d['host_cores']['lanes_run'], round(d['value'] / 1e6, 2))
 "
