@@ -83,6 +83,44 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, const MsmCfg& c
   return nar ? d * 2 : d;
 }
 
+// Every digit of s, f(w, d) for w = 0 .. W-1 in order. C = 0: digit_at with the run-time
+// window layout. C = the SRS's c (10, 15, 17, 20 — the window sizes choose_c picks): the
+// layout is a compile-time constant, the loop unrolls and each digit is a funnel shift
+// (v_alignbit_b32) of two known words, a mask and the carry test — ~6 instructions instead
+// of digit_at's ~25 (word select tree, 64-bit shift). The sort kernels extract every digit of
+// every scalar twice (histogram and scatter); k_sort_one does it for a whole commit on one
+// workgroup.
+template <uint32_t C, class F>
+__device__ __forceinline__ void each_digit(const Fr& s, const MsmCfg& cfg, F&& f) {
+  if constexpr (C == 0) {
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < cfg.W; ++w) f(w, digit_at(s, w, cfg, carry));
+  } else {
+    constexpr uint32_t W = (255 + C - 1) / C, NAR = C * W - 255, WN = W - NAR;
+    static_assert(NAR < W, "balanced windows need (C - 1) W <= 255");
+    uint32_t carry = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < W; ++w) {
+      const bool nar = w >= WN;
+      const uint32_t cw = nar ? C - 1 : C;
+      const uint32_t o = nar ? WN * C + (w - WN) * (C - 1) : w * C;
+      const uint32_t wd = o >> 5, sh = o & 31;
+      uint32_t val = sh == 0 ? s.v[wd]
+                             : __builtin_amdgcn_alignbit(wd + 1 < 8 ? s.v[wd + 1 < 8 ? wd + 1 : 7] : 0u,
+                                                         s.v[wd], sh);
+      val &= (1u << cw) - 1u;
+      int d = (int)(val + carry);
+      if (d > (int)(1u << (cw - 1))) {
+        d -= (int)(1u << cw);
+        carry = 1;
+      } else {
+        carry = 0;
+      }
+      f(w, nar ? d * 2 : d);
+    }
+  }
+}
+
 __device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t& i1) {
   const uint32_t per = (len + gridDim.x - 1) / gridDim.x;
   i0 = blockIdx.x * per;
@@ -112,6 +150,7 @@ constexpr uint32_t kLdsBuckets = 32768;
 
 // Pass 1: LDS histogram of this workgroup's digits, written whole to
 // blockhist[slot][blk][b] (no global atomics).
+template <uint32_t C>
 __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cfg,
                                                        uint32_t* __restrict__ blockhist) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
@@ -127,12 +166,10 @@ __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cf
     for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
       bool neg;
       const Fr s = scalar_half(&sc[i], neg);
-      uint32_t carry = 0;
-      for (uint32_t w = 0; w < cfg.W; ++w) {
-        const int d = digit_at(s, w, cfg, carry);
+      each_digit<C>(s, cfg, [&](uint32_t, int d) {
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;  // wraps for d == 0
         if (d != 0 && b < nb) atomicAdd(&hist[b], 1u);
-      }
+      });
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) out[b0 + b] = hist[b];
@@ -245,6 +282,7 @@ __global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restric
 
 // Pass 2: this workgroup's positions start at offsets[b] + blockhist[slot][blk][b]; each
 // digit takes the next one with an LDS atomic (bucket windows as in k_hist).
+template <uint32_t C>
 __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg cfg,
                                                           uint64_t n_srs,
                                                           const uint32_t* __restrict__ offsets,
@@ -266,15 +304,13 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
     for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
       bool neg;
       const Fr s = scalar_half(&sc[i], neg);
-      uint32_t carry = 0;
-      for (uint32_t w = 0; w < cfg.W; ++w) {
-        const int d = digit_at(s, w, cfg, carry);
+      each_digit<C>(s, cfg, [&](uint32_t w, int d) {
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;
         if (d != 0 && b < nb) {
           const uint32_t pos = atomicAdd(&hist[b], 1u);
           out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
         }
-      }
+      });
     }
     __syncthreads();
   }
@@ -430,6 +466,7 @@ __global__ void __launch_bounds__(1024) k_sort_small(uint32_t* __restrict__ bloc
 // per slot) through one workgroup re-reading the scalars for the scatter: no faster
 // (profiles/r04_sort_one_big_ab.jsonl; removed in round 5).
 constexpr uint32_t kSortOneMax = 8192;  // scalars per slot held in registers
+template <uint32_t C>
 __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, uint64_t n_srs,
                                                    uint32_t chunk, uint32_t* __restrict__ sorted,
                                                    uint64_t sorted_stride,
@@ -458,11 +495,9 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   Fr sv[kPer];
   bool sneg[kPer];
   auto hist_digits = [&](const Fr& x) {
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(x, w, cfg, carry);
+    each_digit<C>(x, cfg, [&](uint32_t, int d) {
       if (d != 0) atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
-    }
+    });
   };
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
@@ -529,14 +564,12 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   }
   __syncthreads();
   auto scatter_digits = [&](const Fr& x, bool neg, uint32_t i) {
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(x, w, cfg, carry);
+    each_digit<C>(x, cfg, [&](uint32_t w, int d) {
       if (d != 0) {
         const uint32_t pos = atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
         out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
       }
-    }
+    });
   };
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter, one workgroup)
@@ -622,6 +655,7 @@ __device__ __forceinline__ void block_scan_excl(uint32_t (&v)[K], uint32_t (&tot
 }
 
 // Wide pass 1: per-workgroup histogram of the coarse bins (bucket >> kFineBits), written whole
+template <uint32_t C>
 __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg cfg, uint32_t NC,
                                                         uint32_t fb, uint32_t* __restrict__ blockhist) {
   __shared__ uint32_t hist[kCoarseMax];
@@ -634,12 +668,10 @@ __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg c
   for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     bool neg;
     const Fr s = scalar_half(&sc[i], neg);
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg, carry);
+    each_digit<C>(s, cfg, [&](uint32_t, int d) {
       const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
       if (b < cfg.B) atomicAdd(&hist[b >> fb], 1u);
-    }
+    });
   }
   __syncthreads();
   uint32_t* out = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * NC;
@@ -649,6 +681,7 @@ __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg c
 // Wide pass 2 (after k_block_scan over the bins): every workgroup scans the bin totals into
 // bin offsets (workgroup 0 also stores them), then each digit's (code, bucket) takes the next
 // slot of its bin in this workgroup's range.
+template <uint32_t C>
 __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCfg cfg, uint32_t NC,
                                                            uint32_t fb, uint64_t n_srs,
                                                            const uint32_t* __restrict__ ccounts,
@@ -689,15 +722,13 @@ __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCf
   for (uint32_t i = i0 + tid; i < i1; i += blockDim.x) {
     bool neg;
     const Fr s = scalar_half(&sc[i], neg);
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < cfg.W; ++w) {
-      const int d = digit_at(s, w, cfg, carry);
+    each_digit<C>(s, cfg, [&](uint32_t w, int d) {
       const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
       if (b < cfg.B) {
         const uint32_t pos = atomicAdd(&hist[b >> fb], 1u);
         out[pos] = make_uint2((uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u), b);
       }
-    }
+    });
   }
 }
 
@@ -1230,6 +1261,17 @@ static G1xyzz rx_to_r_domain(const G1xyzz& p) {
   return r;
 }
 
+// STMT with CC = the SRS's window size as a compile-time constant for the sizes choose_c
+// picks (each_digit's unrolled form), 0 (run-time layout) otherwise
+#define PLK_BY_C(c_, ...)                          \
+  switch (c_) {                                    \
+    case 10: { constexpr uint32_t CC = 10; __VA_ARGS__; } break; \
+    case 15: { constexpr uint32_t CC = 15; __VA_ARGS__; } break; \
+    case 17: { constexpr uint32_t CC = 17; __VA_ARGS__; } break; \
+    case 20: { constexpr uint32_t CC = 20; __VA_ARGS__; } break; \
+    default: { constexpr uint32_t CC = 0; __VA_ARGS__; } break;  \
+  }
+
 int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStream_t stream) {
   const bool same_shape = w.cap_c == s->c && w.cap_windows == s->windows;
   if (same_shape && len <= w.cap_len && slots <= w.cap_slots && w.cap_len) return PLK_OK;
@@ -1291,10 +1333,11 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
   if (!w.ev0) PLK_HIP_TRY(hipEventCreate(&w.ev0));
   if (!w.ev1) PLK_HIP_TRY(hipEventCreate(&w.ev1));
   const int lds = (int)(std::min<uint32_t>((uint32_t)B, kLdsBuckets) * 4);
-  PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-  PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scatter),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  PLK_BY_C(s->c,
+           PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist<CC>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+           PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scatter<CC>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds)))
   w.cap_len = len;
   w.cap_slots = slots;
   w.cap_chunk_min = chunk_min;
@@ -1403,18 +1446,20 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   }
   if (wide) {
     if (max_len) {
-      hipLaunchKernelGGL(k_chist, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
-                         cfg, NC, fb, w.blockhist.as<uint32_t>());
+      PLK_BY_C(s->c, hipLaunchKernelGGL(k_chist<CC>, dim3(hist_blocks, slots), dim3(kHistThreads), 0,
+                                        stream, batch, cfg, NC, fb, w.blockhist.as<uint32_t>()))
     } else {
       PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * NC * 4, stream));
     }
     hipLaunchKernelGGL(k_block_scan, dim3(cdiv(NC, 256), slots), dim3(256), 0, stream,
                        w.blockhist.as<uint32_t>(), hist_blocks, NC, w.counts.as<uint32_t>(),
                        w.len_cur.as<uint32_t>(), w.len_fill.as<uint32_t>());
-    hipLaunchKernelGGL(k_cscatter, dim3(hist_blocks, slots), dim3(kHistThreads), 0, stream, batch,
-                       cfg, NC, fb, (uint64_t)s->n, (const uint32_t*)w.counts.as<uint32_t>(),
-                       (const uint32_t*)w.blockhist.as<uint32_t>(), w.coarse_off.as<uint32_t>(),
-                       w.tmp.as<uint2>(), (uint64_t)(w.sorted_stride - 1));
+    PLK_BY_C(s->c, hipLaunchKernelGGL(k_cscatter<CC>, dim3(hist_blocks, slots), dim3(kHistThreads),
+                                      0, stream, batch, cfg, NC, fb, (uint64_t)s->n,
+                                      (const uint32_t*)w.counts.as<uint32_t>(),
+                                      (const uint32_t*)w.blockhist.as<uint32_t>(),
+                                      w.coarse_off.as<uint32_t>(), w.tmp.as<uint2>(),
+                                      (uint64_t)(w.sorted_stride - 1)))
 #define PLK_FINE_LAUNCH(FB)                                                                       \
   do {                                                                                            \
     hipLaunchKernelGGL(k_fine<FB>, dim3(NC, slots), dim3(1u << FB), 0, stream, B, NC, chunk,      \
@@ -1436,15 +1481,16 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     else PLK_FINE_LAUNCH(8);
 #undef PLK_FINE_LAUNCH
   } else if (sort_one) {
-    hipLaunchKernelGGL(k_sort_one, dim3(1, slots), dim3(1024), 0, stream, batch, cfg,
-                       (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,
-                       w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
-                       (uint64_t)w.task_stride, hdr_dev->flag, gen);
+    PLK_BY_C(s->c, hipLaunchKernelGGL(k_sort_one<CC>, dim3(1, slots), dim3(1024), 0, stream, batch,
+                                      cfg, (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(),
+                                      (uint64_t)w.sorted_stride, w.offsets.as<uint32_t>(),
+                                      w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
+                                      (uint64_t)w.task_stride, hdr_dev->flag, gen))
   } else {
     const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
     if (max_len) {
-      hipLaunchKernelGGL(k_hist, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream, batch,
-                         cfg, w.blockhist.as<uint32_t>());
+      PLK_BY_C(s->c, hipLaunchKernelGGL(k_hist<CC>, dim3(hist_blocks, slots), dim3(kHistThreads), lds,
+                                        stream, batch, cfg, w.blockhist.as<uint32_t>()))
     } else {
       PLK_HIP_TRY(hipMemsetAsync(w.blockhist.ptr, 0, (size_t)slots * hist_blocks * B * 4, stream));
     }
@@ -1463,10 +1509,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
                          w.len_cur.as<uint32_t>());
     }
     if (max_len) {
-      hipLaunchKernelGGL(k_scatter, dim3(hist_blocks, slots), dim3(kHistThreads), lds, stream,
-                         batch, cfg, (uint64_t)s->n, w.offsets.as<uint32_t>(),
-                         w.blockhist.as<uint32_t>(), w.sorted.as<uint32_t>(),
-                         (uint64_t)w.sorted_stride);
+      PLK_BY_C(s->c, hipLaunchKernelGGL(k_scatter<CC>, dim3(hist_blocks, slots), dim3(kHistThreads),
+                                        lds, stream, batch, cfg, (uint64_t)s->n,
+                                        w.offsets.as<uint32_t>(), w.blockhist.as<uint32_t>(),
+                                        w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride))
     }
     if (!small_sort) {
       hipLaunchKernelGGL(k_make_tasks, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
