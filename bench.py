@@ -55,7 +55,13 @@ MADS_PER_MIXED_ADD = 8 * 196 + 2 * 105 + 9 * 196
 _ISA = {}
 
 
-def compiled_loop(kernel: str = "k_accumulateILb0E") -> dict:
+# k_accumulate's two instantiations (csrc/msm_acc.hip k_accumulate<HAS_INF, LONE>): prover
+# lanes run the grouped-product form at 2 waves per SIMD, lone commits the plain chains at 3
+ACC_LANE = ("k_accumulateILb0ELb0E", "k_accumulate<false, false>")
+ACC_LONE = ("k_accumulateILb0ELb1E", "k_accumulate<false, true>")
+
+
+def compiled_loop(kernel: str = ACC_LANE[0]) -> dict:
     """The kernel's loop body as compiled (largest basic block of its gfx950 code in
     libplk.so, tools/isa_count.py): v_mad_u64_u32 count, instruction count and the VALU issue
     cycles of the mix at the measured per-instruction costs (tools/ubench_issue.hip)."""
@@ -562,12 +568,13 @@ def host_info():
     return {"nproc": os.cpu_count(), "usable_cores": usable, "cpu_model": model}
 
 
-def valu_roofline(adds_per_s):
+def valu_roofline(adds_per_s, form=ACC_LANE):
     """k_accumulate against its binding ceiling, VALU issue: each mixed addition's compiled
-    instruction mix priced at the measured per-instruction issue costs, per wave of 64
-    additions, against every SIMD issuing every cycle (SIMD-cycles/s). The v_mad_u64_u32 rate
-    against its own measured peak is kept beside it."""
-    isa = compiled_loop()
+    instruction mix (of the instantiation that ran: `form`) priced at the measured
+    per-instruction issue costs, per wave of 64 additions, against every SIMD issuing every
+    cycle (SIMD-cycles/s). The v_mad_u64_u32 rate against its own measured peak is kept beside
+    it."""
+    isa = compiled_loop(form[0])
     achieved = adds_per_s / 64.0 * isa["valu_cycles"]
     mads = adds_per_s * isa["v_mad_u64_u32"]
     return {"bound": "valu", "achieved": achieved, "peak": SIMD_CYCLES_PEAK,
@@ -579,6 +586,7 @@ def valu_roofline(adds_per_s):
             "instructions_per_point_add": isa["instructions"],
             "valu_instructions_per_point_add": isa.get("valu_instructions"),
             "s_nop_per_point_add": isa.get("s_nop"), "mads_source": isa["source"],
+            "kernel_form": form[1],
             "mad": {"achieved": mads, "peak": VALU_MAD_PEAK, "unit": "mad/s",
                     "frac": mads / VALU_MAD_PEAK, "peak_source": VALU_MAD_PEAK_SOURCE}}
 
@@ -644,7 +652,7 @@ def cpu_threads(args) -> int:
     return host_info()["usable_cores"] or 1
 
 
-def acc_roofline(ms_total, launches, adds, points, label):
+def acc_roofline(ms_total, launches, adds, points, label, form=ACC_LANE):
     """k_accumulate: algorithmic bytes (128 B per MSM point) and mixed additions
     per launch over the average launch duration (dispatch-stamped events)."""
     ms = ms_total / launches
@@ -654,7 +662,7 @@ def acc_roofline(ms_total, launches, adds, points, label):
             "achieved_gbs": alg / (ms * 1e-3) / 1e9,
             "point_adds_per_launch": adds / launches,
             "point_adds_per_s": adds / (ms_total * 1e-3),
-            "valu": valu_roofline(adds / (ms_total * 1e-3)), "timing": label}
+            "valu": valu_roofline(adds / (ms_total * 1e-3), form), "timing": label}
 
 
 def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
@@ -795,8 +803,8 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
         inw = (acc_roofline(acc_ms, launches, adds, points, "all lanes inside the timed region; "
                             "durations overlap other lanes' kernels (not the kernel's own time)")
                if launches and acc_ms > 0 else None)
-        traffic = load_pmc_traffic("k_accumulate")
-        traffic2 = load_pmc_traffic("k_accumulate", "hbm_bytes_per_launch_stream_corrected")
+        traffic = load_pmc_traffic(ACC_LANE[1])
+        traffic2 = load_pmc_traffic(ACC_LANE[1], "hbm_bytes_per_launch_stream_corrected")
         roof = binding_roofline(solo["valu"], solo["achieved_gbs"],
                                 solo["algorithmic_bytes_per_launch"], traffic, "k_accumulate")
         roof.update({
@@ -975,8 +983,8 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
         adds = sum(e[1] for e in ev) / steps
         alg_bytes = 128.0 * n  # N * (32 B scalar + 96 B base)
         gbs = alg_bytes / (launch_ms * 1e-3) / 1e9
-        roof = binding_roofline(valu_roofline(adds / (launch_ms * 1e-3)), gbs, alg_bytes,
-                                load_pmc_traffic("k_accumulate", fname=f"pmc_traffic_msm{k}.json"),
+        roof = binding_roofline(valu_roofline(adds / (launch_ms * 1e-3), ACC_LONE), gbs, alg_bytes,
+                                load_pmc_traffic(ACC_LONE[1], fname=f"pmc_traffic_msm{k}.json"),
                                 "k_accumulate")
         roof.update({"avg_launch_ms": launch_ms, "point_adds_per_launch": adds,
                      "point_adds_per_s": adds / (launch_ms * 1e-3),
@@ -1166,7 +1174,7 @@ def main():
         alg_bytes = 2.0 * 8 * n * 32  # one read + one write of the 8n vector
         kname = "k_ntt_pass"
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic(kname)
+    traffic = load_pmc_traffic(ACC_LONE[1] if kname == "k_accumulate" else kname)
     result = {
         "metric": "PLONK prover constraints/sec (BLS12-381) at n=2^16 and 2^20, 1/2/4/8 GPUs",
         "value": n * steps * (1 if shard else world) / elapsed,
@@ -1207,8 +1215,8 @@ def main():
             "note": "integer-VALU-bound path (no MFMA); HBM is the secondary roofline"}
     if kname == "k_accumulate" and acc:  # the binding (VALU issue) roofline at top level
         adds = sum(hp.msm_adds) / len(hp.msm_adds)
-        roof = binding_roofline(valu_roofline(adds / (launch_ms * 1e-3)), achieved, alg_bytes,
-                                traffic, kname)
+        roof = binding_roofline(valu_roofline(adds / (launch_ms * 1e-3), ACC_LONE), achieved,
+                                alg_bytes, traffic, kname)
         roof.update({"avg_launch_ms": launch_ms, "point_adds_per_launch": adds,
                      "point_adds_per_s": adds / (launch_ms * 1e-3),
                      "note": "integer-VALU-bound (no MFMA); HBM is the secondary roofline"})

@@ -79,10 +79,15 @@ def test_compiled_loop_mads():
     libplk.so (tools/isa_count.py), not from the formula constant."""
     sys.path.insert(0, str(ROOT))
     import bench
-    isa = bench.compiled_loop()
-    assert "compiled" in isa["source"], isa
-    assert 3000 < isa["v_mad_u64_u32"] < isa["instructions"] < 6000
-    assert isa["v_mad_u64_u32"] * 4 < isa["valu_cycles"] < isa["instructions"] * 5
+    for form in (bench.ACC_LANE, bench.ACC_LONE):  # both k_accumulate instantiations
+        isa = bench.compiled_loop(form[0])
+        assert "compiled" in isa["source"], (form, isa)
+        assert 3000 < isa["v_mad_u64_u32"] < isa["instructions"] < 6000
+        assert isa["v_mad_u64_u32"] * 4 < isa["valu_cycles"] < isa["instructions"] * 5
+    # the lane form's interleaved product groups: fewer VALU instructions than the plain chains
+    lane, lone = bench.compiled_loop(bench.ACC_LANE[0]), bench.compiled_loop(bench.ACC_LONE[0])
+    assert lane["v_mad_u64_u32"] == lone["v_mad_u64_u32"]
+    assert lane["valu_instructions"] < lone["valu_instructions"]
 
 
 def test_gpus_flag_must_match_launcher():
