@@ -15,6 +15,7 @@
 //
 // HBM traffic per transform: P * 2 * N * 32 B (P = 3 at N = 2^20..2^24).
 #include <cstdlib>
+#include <type_traits>
 
 #include "ffr.hpp"
 #include "internal.hpp"
@@ -216,6 +217,11 @@ __device__ __forceinline__ void twmul2(const RFr& a0, uint32_t i0, const RFr& a1
 // Two radix-2 DIF stages (halves 2h and h) on rows x0..x3 = j, j+h, j+2h, j+3h of one
 // column (r = j mod h); outputs o0..o3 belong at rows j, j+h, j+2h, j+3h. Inputs normalised,
 // < 5r; outputs normalised, < 4r.
+// H1: h == 1, as a template parameter: with a run-time `h == 1` branch assigning the outputs
+// on both paths the compiler merged them through an 80-byte scratch object (76 B per lane in
+// every k_ntt_pass instantiation: 18 stores and 18 loads per step), so the callers branch
+// once per step loop instead.
+template <bool H1>
 __device__ __forceinline__ void r4_math(const uint32_t* twl, uint32_t TS, const uint32_t* ztab,
                                         uint32_t r, uint32_t h, uint32_t sh1, uint32_t sh2,
                                         const RFr& x0, const RFr& x1, const RFr& x2,
@@ -223,7 +229,7 @@ __device__ __forceinline__ void r4_math(const uint32_t* twl, uint32_t TS, const 
   // inputs: normalised, < 5r. Stage of half 2h: twiddle w^(r s1) for x0/x2 (identity
   // when r = 0), w^((r+h) s1) for x1/x3; sums y0, y1 unnormalised (limbs < 2^30, < 10r)
   const RFr y0 = add_u(x0, x2), y1 = add_u(x1, x3);
-  if (h == 1) {  // r = 0 in every group: no twiddle on x0 / x2 nor in the second stage
+  if constexpr (H1) {  // r = 0 in every group: no twiddle on x0 / x2 nor in the second stage
     const RFr y2 = reduce_q(rx_sub_u<FrCfg, 6>(x0, x2), ztab);  // < 4r
     const RFr y3 = twmul(rx_sub_u<FrCfg, 6>(x1, x3), twl, TS, 1u << sh1);  // < 3r
     o0 = reduce_q(add_u(y0, y1), ztab);             // < 20r -> < 4r
@@ -248,14 +254,14 @@ __device__ __forceinline__ void r4_math(const uint32_t* twl, uint32_t TS, const 
 }
 
 // r4_math, outputs stored back to LDS at i0..i3
-template <uint32_t DS>
+template <uint32_t DS, bool H1>
 __device__ __forceinline__ void r4_step(uint32_t* data, const uint32_t* twl, uint32_t TS,
                                         const uint32_t* ztab, uint32_t r, uint32_t h,
                                         uint32_t sh1, uint32_t sh2, uint32_t i0, uint32_t i1,
                                         uint32_t i2, uint32_t i3, const RFr& x0, const RFr& x1,
                                         const RFr& x2, const RFr& x3) {
   RFr o0, o1, o2, o3;
-  r4_math(twl, TS, ztab, r, h, sh1, sh2, x0, x1, x2, x3, o0, o1, o2, o3);
+  r4_math<H1>(twl, TS, ztab, r, h, sh1, sh2, x0, x1, x2, x3, o0, o1, o2, o3);
   lds_std<DS>(data, i0, o0);
   lds_std<DS>(data, i2, o2);
   lds_std<DS>(data, i1, o1);
@@ -454,10 +460,10 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
         RFr x0 = lds_ldd<DS>(data, (j << lt) + t), x1 = lds_ldd<DS>(data, ((j + 4) << lt) + t);
         RFr x2 = lds_ldd<DS>(data, ((j + 8) << lt) + t), x3 = lds_ldd<DS>(data, ((j + 12) << lt) + t);
         RFr o0, o1, o2, o3;
-        r4_math(twl, TS, ztab, r, 4, lr - 4, lr - 3, x0, x1, x2, x3, o0, o1, o2, o3);
+        r4_math<false>(twl, TS, ztab, r, 4, lr - 4, lr - 3, x0, x1, x2, x3, o0, o1, o2, o3);
         quad_transpose(o0, o1, o2, o3);  // lane r now holds rows 16B + 4r + (0, 1, 2, 3)
         const uint32_t jq = (B << 4) + (r << 2);
-        r4_step<DS>(data, twl, TS, ztab, 0, 1, lr - 2, lr - 1, (jq << lt) + t,
+        r4_step<DS, true>(data, twl, TS, ztab, 0, 1, lr - 2, lr - 1, (jq << lt) + t,
                     ((jq + 1) << lt) + t, ((jq + 2) << lt) + t, ((jq + 3) << lt) + t, o0, o1, o2,
                     o3);
       }
@@ -465,16 +471,20 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
       __syncthreads();
       continue;
     }
-    for (uint32_t g = tid; g < (E >> 2); g += bd) {
-      const uint32_t t = g & (T - 1), jg = g >> lt;
-      const uint32_t r = jg & (h - 1);
-      const uint32_t j = ((jg >> (lh - 1)) << (lh + 1)) + r;
-      const uint32_t i0 = (j << lt) + t, i1 = ((j + h) << lt) + t;
-      const uint32_t i2 = ((j + 2 * h) << lt) + t, i3 = ((j + 3 * h) << lt) + t;
-      const RFr x0 = lds_ldd<DS>(data, i0), x1 = lds_ldd<DS>(data, i1);
-      const RFr x2 = lds_ldd<DS>(data, i2), x3 = lds_ldd<DS>(data, i3);
-      r4_step<DS>(data, twl, TS, ztab, r, h, sh1, sh2, i0, i1, i2, i3, x0, x1, x2, x3);
-    }
+    auto steps = [&](auto h1) {
+      for (uint32_t g = tid; g < (E >> 2); g += bd) {
+        const uint32_t t = g & (T - 1), jg = g >> lt;
+        const uint32_t r = jg & (h - 1);
+        const uint32_t j = ((jg >> (lh - 1)) << (lh + 1)) + r;
+        const uint32_t i0 = (j << lt) + t, i1 = ((j + h) << lt) + t;
+        const uint32_t i2 = ((j + 2 * h) << lt) + t, i3 = ((j + 3 * h) << lt) + t;
+        const RFr x0 = lds_ldd<DS>(data, i0), x1 = lds_ldd<DS>(data, i1);
+        const RFr x2 = lds_ldd<DS>(data, i2), x3 = lds_ldd<DS>(data, i3);
+        r4_step<DS, decltype(h1)::value>(data, twl, TS, ztab, r, h, sh1, sh2, i0, i1, i2, i3, x0, x1, x2, x3);
+      }
+    };
+    if (h == 1) steps(std::true_type{});
+    else steps(std::false_type{});
     __syncthreads();
   }
   if (lh == 0) {  // odd radix: last stage of half 1 (twiddle-free)

@@ -544,8 +544,17 @@ __global__ void __launch_bounds__(kRuffiniThreads) k_ruffini_single(const Fr* __
                                                                     Fr ziE, Fr* __restrict__ q) {
   __shared__ Fr T[kRuffiniThreads], U[kRuffiniThreads];
   const uint32_t tid = threadIdx.x;
-  T[tid] = tid ? zE : rx_pack(rx_one<FrCfg>());
-  U[tid] = tid ? ziE : zi;
+  // word by word: a select between two by-value argument structs took their addresses and
+  // staged both in scratch memory (80 B per lane)
+  const Fr one = rx_pack(rx_one<FrCfg>());
+  Fr t0, u0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    t0.v[i] = tid ? zE.v[i] : one.v[i];
+    u0.v[i] = tid ? ziE.v[i] : zi.v[i];
+  }
+  T[tid] = t0;
+  U[tid] = u0;
   __syncthreads();
   for (uint32_t h = 1; h < kRuffiniThreads; h <<= 1) {  // inclusive product scans
     const RFr a = tid >= h ? rx_unpack(T[tid - h]) : rx_one<FrCfg>();
