@@ -26,7 +26,11 @@ namespace {
 
 constexpr uint32_t kMaxLr = 9;   // radix up to 512 (PLK_NTT_MAX_LR: up to kMaxLrHard)
 constexpr uint32_t kMaxLrHard = 10;
-constexpr uint32_t kMaxLe = 10;  // 1024 elements (32 KiB) per workgroup
+// 1024 elements (32 KiB) per workgroup. Round 5: 512-element tiles (twice the workgroups, 22
+// KiB of LDS each, so that more tiles are resident and their load / store phases stagger)
+// measured slower: dft + idft 2^20 0.291 -> 0.323 ms, 2^23 1.99 -> 2.18 ms, 2^20 proofs -1.5 %
+// (profiles/r05_ntt_tile512_ab.jsonl)
+constexpr uint32_t kMaxLe = 10;
 
 __device__ __forceinline__ Fr ld_fr(const Fr* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
