@@ -20,8 +20,12 @@ BUILD = PKG / "build"
 LIB = PKG / "libplk.so"
 ARCH = os.environ.get("PLK_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -Rpass-analysis=kernel-resource-usage: each TU's per-kernel VGPR / scratch / occupancy report
+# is kept next to its object (build/<tu>.res.txt) and checked by tests/test_build_resources.py
+# (round 5: a 76-B scratch object had sat unnoticed in every NTT pass)
+RES_FLAG = "-Rpass-analysis=kernel-resource-usage"
 CFLAGS = ["-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function",
-          f"-I{ROOT / 'include'}"]
+          f"-I{ROOT / 'include'}", RES_FLAG]
 
 
 def _headers():
@@ -40,6 +44,10 @@ def _compile(src: Path, obj: Path, cflags) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+    if RES_FLAG in cflags:  # the device-side resource remarks only
+        keep = ("Function Name", "VGPRs", "AGPRs", "ScratchSize", "Occupancy", "LDS Size")
+        lines = [ln for ln in r.stderr.splitlines() if "remark:" in ln and any(k in ln for k in keep)]
+        obj.with_suffix(".res.txt").write_text("\n".join(lines) + "\n")
     return src.name
 
 

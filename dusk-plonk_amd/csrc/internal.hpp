@@ -155,13 +155,13 @@ struct PinnedBuf {
   ~PinnedBuf() {
     if (ptr) (void)hipHostFree(ptr);
   }
-  int alloc(size_t b) {
+  int alloc(size_t b, unsigned flags = hipHostMallocDefault) {
     if (ptr && bytes >= b) return PLK_OK;
     if (ptr) (void)hipHostFree(ptr);
     ptr = nullptr;
     bytes = 0;
     if (b == 0) return PLK_OK;
-    const hipError_t e = hipHostMalloc(&ptr, b, hipHostMallocDefault);
+    const hipError_t e = hipHostMalloc(&ptr, b, flags);
     if (e != hipSuccess) {
       ptr = nullptr;
       last_hip_error() = e;

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "internal.hpp"
@@ -129,8 +130,8 @@ __device__ __forceinline__ void slot_range(uint32_t len, uint32_t& i0, uint32_t&
 
 // Canonical scalar in [0, (r-1)/2]: s, or r - s with the digit signs flipped (s P = (r - s)(-P)).
 // With s < 2^254 the signed c-bit recoding needs W = ceil(255 / c) windows (c = 17: 15).
-__device__ __forceinline__ Fr scalar_half(const Fr* p, bool& neg) {
-  const Fr s = fe_from_mont(ld_fr(p));
+__device__ __forceinline__ Fr scalar_half_v(const Fr& raw, bool& neg) {
+  const Fr s = fe_from_mont(raw);
   const Fr t = fe_neg(s);
   bool lt = false;  // t < s
 #pragma unroll
@@ -142,6 +143,33 @@ __device__ __forceinline__ Fr scalar_half(const Fr* p, bool& neg) {
   }
   neg = lt;
   return lt ? t : s;
+}
+__device__ __forceinline__ Fr scalar_half(const Fr* p, bool& neg) { return scalar_half_v(ld_fr(p), neg); }
+
+// f(i, canonical half of scalar i, its sign flip) for i = i0 + t, i0 + t + step, ... < i1 in
+// order, with kScalarLoads scalars loaded before the first is processed: the sort passes are
+// bound by load latency (one scalar in flight per thread before), not by bytes
+constexpr uint32_t kScalarLoads = 4;
+template <class F>
+__device__ __forceinline__ void for_scalars(const Fr* __restrict__ sc, uint32_t i0, uint32_t i1,
+                                            uint32_t t, uint32_t step, F&& f) {
+  uint32_t i = i0 + t;
+  for (; i + (kScalarLoads - 1) * step < i1; i += kScalarLoads * step) {
+    Fr raw[kScalarLoads];
+#pragma unroll
+    for (uint32_t u = 0; u < kScalarLoads; ++u) raw[u] = ld_fr(&sc[i + u * step]);
+#pragma unroll
+    for (uint32_t u = 0; u < kScalarLoads; ++u) {
+      bool neg;
+      const Fr s = scalar_half_v(raw[u], neg);
+      f(i + u * step, s, neg);
+    }
+  }
+  for (; i < i1; i += step) {
+    bool neg;
+    const Fr s = scalar_half_v(ld_fr(&sc[i]), neg);
+    f(i, s, neg);
+  }
 }
 
 // LDS histograms cover at most kLdsBuckets buckets (128 KiB); larger bucket sets (c = 17)
@@ -163,14 +191,12 @@ __global__ void __launch_bounds__(kHistThreads) k_hist(MsmBatch batch, MsmCfg cf
     const uint32_t nb = min(kLdsBuckets, B - b0);
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
     __syncthreads();
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-      bool neg;
-      const Fr s = scalar_half(&sc[i], neg);
+    for_scalars(sc, i0, i1, threadIdx.x, blockDim.x, [&](uint32_t, const Fr& s, bool) {
       each_digit<C>(s, cfg, [&](uint32_t, int d) {
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;  // wraps for d == 0
         if (d != 0 && b < nb) atomicAdd(&hist[b], 1u);
       });
-    }
+    });
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) out[b0 + b] = hist[b];
     __syncthreads();
@@ -301,9 +327,7 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
     const uint32_t nb = min(kLdsBuckets, B - b0);
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = off[b0 + b] + bh[b0 + b];
     __syncthreads();
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-      bool neg;
-      const Fr s = scalar_half(&sc[i], neg);
+    for_scalars(sc, i0, i1, threadIdx.x, blockDim.x, [&](uint32_t i, const Fr& s, bool neg) {
       each_digit<C>(s, cfg, [&](uint32_t w, int d) {
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - b0;
         if (d != 0 && b < nb) {
@@ -311,7 +335,7 @@ __global__ void __launch_bounds__(kHistThreads) k_scatter(MsmBatch batch, MsmCfg
           out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
         }
       });
-    }
+    });
     __syncthreads();
   }
 }
@@ -587,8 +611,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
 // (2) one workgroup per bin counting-sorts its entries by bucket inside the bin's own
 // region (LDS counters, writes that stay in one L2), emitting the bucket offsets and the
 // per-bucket task counts on the way; (3) the task records, as k_make_tasks does.
-constexpr uint32_t kFineBits = 10;
-constexpr uint32_t kFine = 1u << kFineBits;  // buckets per coarse bin = threads of k_fine
+constexpr uint32_t kFineBits = 10;  // 2^10 buckets per coarse bin = threads of k_fine
 // A bucket-range part (parts > 1) of 2^(c-1) / parts buckets keeps >= 256 coarse bins (k_fine
 // / k_make_tasks_wide workgroups) with bins of 2^FB buckets, FB = max(8, 10 - log2 parts)
 constexpr uint32_t kFineBitsMin = 8;
@@ -665,14 +688,12 @@ __global__ void __launch_bounds__(kHistThreads) k_chist(MsmBatch batch, MsmCfg c
   const Fr* sc = batch.scalars[slot];
   for (uint32_t b = threadIdx.x; b < NC; b += blockDim.x) hist[b] = 0;
   __syncthreads();
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    bool neg;
-    const Fr s = scalar_half(&sc[i], neg);
+  for_scalars(sc, i0, i1, threadIdx.x, blockDim.x, [&](uint32_t, const Fr& s, bool) {
     each_digit<C>(s, cfg, [&](uint32_t, int d) {
       const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
       if (b < cfg.B) atomicAdd(&hist[b >> fb], 1u);
     });
-  }
+  });
   __syncthreads();
   uint32_t* out = blockhist + ((size_t)slot * gridDim.x + blockIdx.x) * NC;
   for (uint32_t b = threadIdx.x; b < NC; b += blockDim.x) out[b] = hist[b];
@@ -719,9 +740,7 @@ __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCf
   slot_range(batch.len[slot], i0, i1);
   const Fr* sc = batch.scalars[slot];
   uint2* out = tmp + (size_t)slot * tmp_stride;
-  for (uint32_t i = i0 + tid; i < i1; i += blockDim.x) {
-    bool neg;
-    const Fr s = scalar_half(&sc[i], neg);
+  for_scalars(sc, i0, i1, tid, blockDim.x, [&](uint32_t i, const Fr& s, bool neg) {
     each_digit<C>(s, cfg, [&](uint32_t w, int d) {
       const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u - cfg.b_lo;  // d = 0: wraps past B
       if (b < cfg.B) {
@@ -729,13 +748,16 @@ __global__ void __launch_bounds__(kHistThreads) k_cscatter(MsmBatch batch, MsmCf
         out[pos] = make_uint2((uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u), b);
       }
     });
-  }
+  });
 }
 
 // Wide pass 3: one workgroup per (bin, slot), one thread per bucket of the bin. Counting sort
 // of the bin's entries by bucket into its own region of `sorted`; bucket offsets (global),
 // per-bucket task and full-task offsets relative to the bin, the bin's totals and the
 // global histogram of tail lengths (for the execution order of the tasks).
+// loads in flight per thread and pass (8 measured no faster in round 5:
+// profiles/r05_sort_prefetch_readback_ab.jsonl)
+constexpr uint32_t kFineLoads = 4;
 template <uint32_t FB>
 __global__ void __launch_bounds__(1u << FB) k_fine(uint32_t B, uint32_t NC, uint32_t chunk,
                                                 const uint32_t* __restrict__ coarse_off,
@@ -757,14 +779,14 @@ __global__ void __launch_bounds__(1u << FB) k_fine(uint32_t B, uint32_t NC, uint
   cnt[tid] = 0;
   if (tid < kChunkMax) s_len[tid] = 0;
   __syncthreads();
-  {  // 4 loads in flight per thread, then their atomics
+  {  // kFineLoads loads in flight per thread, then their atomics
     uint32_t e = lo + tid;
-    for (; e + 3 * kFine < hi; e += 4 * kFine) {
-      uint32_t k[4];
+    for (; e + (kFineLoads - 1) * kFine < hi; e += kFineLoads * kFine) {
+      uint32_t k[kFineLoads];
 #pragma unroll
-      for (uint32_t u = 0; u < 4; ++u) k[u] = in[e + u * kFine].y;
+      for (uint32_t u = 0; u < kFineLoads; ++u) k[u] = in[e + u * kFine].y;
 #pragma unroll
-      for (uint32_t u = 0; u < 4; ++u) atomicAdd(&cnt[k[u] & (kFine - 1)], 1u);
+      for (uint32_t u = 0; u < kFineLoads; ++u) atomicAdd(&cnt[k[u] & (kFine - 1)], 1u);
     }
     for (; e < hi; e += kFine) atomicAdd(&cnt[in[e].y & (kFine - 1)], 1u);
   }
@@ -787,15 +809,15 @@ __global__ void __launch_bounds__(1u << FB) k_fine(uint32_t B, uint32_t NC, uint
   __syncthreads();
   uint32_t* out = sorted + (size_t)slot * sorted_stride + lo;
   uint32_t e = lo + tid;
-  for (; e + 3 * kFine < hi; e += 4 * kFine) {
-    uint2 x[4];
-    uint32_t pos[4];
+  for (; e + (kFineLoads - 1) * kFine < hi; e += kFineLoads * kFine) {
+    uint2 x[kFineLoads];
+    uint32_t pos[kFineLoads];
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) x[u] = in[e + u * kFine];
+    for (uint32_t u = 0; u < kFineLoads; ++u) x[u] = in[e + u * kFine];
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) pos[u] = atomicAdd(&cnt[x[u].y & (kFine - 1)], 1u);
+    for (uint32_t u = 0; u < kFineLoads; ++u) pos[u] = atomicAdd(&cnt[x[u].y & (kFine - 1)], 1u);
 #pragma unroll
-    for (uint32_t u = 0; u < 4; ++u) out[pos[u]] = x[u].x;
+    for (uint32_t u = 0; u < kFineLoads; ++u) out[pos[u]] = x[u].x;
   }
   for (; e < hi; e += kFine) {
     const uint2 x = in[e];
@@ -1321,13 +1343,18 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
     if ((st = w.done.alloc(kMaxSlots * sizeof(uint32_t)))) return st;
     if (w.done.ptr != before) PLK_HIP_TRY(hipMemsetAsync(w.done.ptr, 0, kMaxSlots * sizeof(uint32_t), stream));
   }
-  {  // readback record: header (flags, entry counts) then the bit sums (nout <= 32 per slot)
-    void* before = w.bits2.ptr;
-    if ((st = w.bits2.alloc(sizeof(ReadbackHeader) + (size_t)kMaxSlots * 32 * sizeof(G1xyzz))))
+  {  // readback record: header (flags, entry counts) then the bit sums (nout <= 32 per slot),
+     // in coherent mapped host memory (round 5: the per-batch copy dispatch it replaces cost
+     // small proofs a dispatch per commit group). The previous batch has completed (every
+     // batch ends with a host wait), so the host may clear it.
+    void* before = w.host_out.ptr;
+    if ((st = w.host_out.alloc(sizeof(ReadbackHeader) + (size_t)kMaxSlots * 32 * sizeof(G1xyzz),
+                               hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable)))
       return st;
-    if (w.bits2.ptr != before) {  // fresh memory: the flags start at generation 0
-      PLK_HIP_TRY(hipMemsetAsync(w.bits2.ptr, 0, sizeof(ReadbackHeader), stream));
+    if (w.host_out.ptr != before) {  // fresh memory: the flags start at generation 0
+      std::memset(w.host_out.ptr, 0, sizeof(ReadbackHeader));
       w.gen = 0;
+      PLK_HIP_TRY(hipHostGetDevicePointer(&w.out_dev, w.host_out.ptr, 0));
     }
   }
   if (!w.ev0) PLK_HIP_TRY(hipEventCreate(&w.ev0));
@@ -1431,10 +1458,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   const uint32_t hist_blocks =
       std::max<uint32_t>(1, std::min<uint32_t>(kHistBlocksMax, cdiv(max_len, 512)));
 
-  ReadbackHeader* hdr_dev = w.bits2.as<ReadbackHeader>();
+  ReadbackHeader* hdr_dev = static_cast<ReadbackHeader*>(w.out_dev);
   G1xyzz* bits_dev = reinterpret_cast<G1xyzz*>(hdr_dev + 1);
   if (++w.gen == 0xFFFFFFFFu) {  // wrap: clear the stamps once every 2^32 - 1 batches
-    PLK_HIP_TRY(hipMemsetAsync(hdr_dev, 0, sizeof(ReadbackHeader), stream));
+    std::memset(w.host_out.ptr, 0, sizeof(ReadbackHeader));
     w.gen = 1;
   }
   const uint32_t gen = w.gen;
@@ -1570,13 +1597,10 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   else bitsum_launch<false, false>(wide, G, slots, NR, B, w, fold, nbits, nout, bits_dev, hdr_dev, stream);
   PLK_HIP_TRY(hipGetLastError());
 
-  // ONE copy of the readback record: flags, entry counts, then the slots' bit sums
-  const size_t t_count = (size_t)slots * nout;
-  const size_t rec_bytes = sizeof(ReadbackHeader) + t_count * sizeof(G1xyzz);
-  if ((st = w.host_out.alloc(rec_bytes))) return st;
+  // the readback record (flags, entry counts, then the slots' bit sums) is in host memory
+  // once the batch's kernels have completed
   const ReadbackHeader* hdr = w.host_out.as<ReadbackHeader>();
   const G1xyzz* T = reinterpret_cast<const G1xyzz*>(hdr + 1);
-  PLK_HIP_TRY(hipMemcpyAsync(w.host_out.ptr, hdr_dev, rec_bytes, hipMemcpyDeviceToHost, stream));
   PLK_HIP_TRY(stream_wait(stream));
   const uint32_t* ent = hdr->entries;
   uint32_t flag[kMaxSlots];

@@ -89,8 +89,8 @@ __device__ __forceinline__ Fr ld_fr(const Fr* p) {
 
 inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-// Head of a batch's readback record (device buffer MsmWorkspace::bits2, copied to the host
-// in one piece with the bit sums that follow it): per slot the degree-check flag (stamped
+// Head of a batch's readback record (MsmWorkspace::host_out, written by the kernels straight
+// into mapped host memory, the bit sums after it): per slot the degree-check flag (stamped
 // with the batch's generation number by k_any_nonzero) and the entry count (point
 // additions, written by k_bitsum2). 128 bytes, so the G1xyzz records after it stay aligned.
 struct ReadbackHeader {
@@ -100,12 +100,14 @@ struct ReadbackHeader {
 static_assert(sizeof(ReadbackHeader) % 16 == 0, "alignment of the bit sums");
 
 struct MsmWorkspace {
-  DevBuf counts, blockhist, offsets, task_off, full_off, len_cur, sorted, tasks, partials, bsum, bits1,
-      bits2;
+  DevBuf counts, blockhist, offsets, task_off, full_off, len_cur, sorted, tasks, partials, bsum, bits1;
   // wide bucket sets only (msm.hip: two-level sort, run-sum reduction)
   DevBuf tmp, task_rel, bin_tot, len_fill, coarse_off, rsum, ys, zs;
   DevBuf done;  // k_bitsum1's per-slot arrival counters (its fold of k_bitsum2)
-  PinnedBuf host_out;  // the readback record (ReadbackHeader + bit sums) on the host
+  // the readback record (ReadbackHeader + bit sums): coherent host memory mapped into the
+  // device's address space, written by the kernels themselves (no copy dispatch per batch)
+  PinnedBuf host_out;
+  void* out_dev = nullptr;  // host_out's device address
   uint32_t gen = 0;    // generation number of the last batch (degree-check flag stamps)
   size_t cap_len = 0, task_stride = 0, sorted_stride = 0;
   uint32_t cap_slots = 0;

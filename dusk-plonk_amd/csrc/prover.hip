@@ -1037,7 +1037,11 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     TRY(P->w_coef.alloc((5 * n + S) * sizeof(Fr)));
     TRY(P->tmp_a.alloc(5 * n * sizeof(Fr)));
     TRY(P->eval_partial.alloc((size_t)kMaxEval * pk_eval_max_blocks(nq) * sizeof(Fr)));
-    TRY(P->eval_out.alloc(kMaxEval * sizeof(Fr)));
+    if (!P->eval_out.ptr) {
+      TRY(P->eval_out.alloc(kMaxEval * sizeof(Fr),
+                            hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+      PLK_HIP_TRY(hipHostGetDevicePointer(&P->eval_dev, P->eval_out.ptr, 0));
+    }
     // 4 nq: the four wires' 12 coset blocks transform in one batch (24n of scratch: the output
     // doubles as the other ping-pong buffer, ntt_run_batch)
     TRY(P->ntt_scratch.alloc(4 * nq * sizeof(Fr)));
@@ -1137,9 +1141,8 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     const Fr fixed_sep = tr.challenge_scalar("fixed base separation challenge");
     const Fr var_sep = tr.challenge_scalar("variable base separation challenge");
     Fr* pil = P->pi_lag.as<Fr>();
-    // pin_small: [0, #pi) PI values uploaded here, [#pi, #pi + kMaxEval) the evaluations
-    // read back in round 4 (sized once: queued copies keep pointing into it)
-    TRY(P->pin_small.alloc((pis.size() + kMaxEval) * sizeof(Fr)));
+    // pin_small: the PI values uploaded here (sized once: queued copies keep pointing into it)
+    TRY(P->pin_small.alloc(std::max<size_t>(pis.size(), 1) * sizeof(Fr)));
     // PI(X) = idft of the public-input vector (prover.rs:229): for a few public inputs
     // straight from its definition, one product per input and coefficient (no upload, no
     // transform); otherwise the vector is uploaded and transformed
@@ -1333,12 +1336,11 @@ int plk_prover_prove(plk_prover* P, const plk_composer* cs, uint64_t seed, plk_p
     if (key->has_var) rterm(qc + QVAR * n, n, -1);
     rterm(zc, n + 3, -1);
     rterm(sc + 3 * n, n, -1);
-    TRY(pk_eval(eb, ne, 3 * n + t4_len, P->eval_partial.as<Fr>(), P->eval_out.as<Fr>(), s));
+    // the evaluations land in host memory (no copy dispatch): read once the stream is done
+    TRY(pk_eval(eb, ne, 3 * n + t4_len, P->eval_partial.as<Fr>(), static_cast<Fr*>(P->eval_dev), s));
     Fr evs[kMaxEval];
-    Fr* evs_pin = P->pin_small.as<Fr>() + pis.size();
-    PLK_HIP_TRY(hipMemcpyAsync(evs_pin, P->eval_out.ptr, ne * sizeof(Fr), hipMemcpyDeviceToHost, s));
     PLK_HIP_TRY(stream_wait(s));
-    std::memcpy(evs, evs_pin, ne * sizeof(Fr));
+    std::memcpy(evs, P->eval_out.ptr, ne * sizeof(Fr));
     const Fr t_eval = evs[0], a_e = evs[1], b_e = evs[2], c_e = evs[3], d_e = evs[4];
     const Fr s1_e = evs[5], s2_e = evs[6], s3_e = evs[7];
     const Fr qar_e = evs[8], qc_e = evs[9], ql_e = evs[10], qr_e = evs[11];

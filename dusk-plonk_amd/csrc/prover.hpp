@@ -271,7 +271,10 @@ struct plk_prover {
   void* allgather_user = nullptr;
   // per-proof scratch
   plk::PinnedBuf pin_witness, pin_small;  // host staging of the witness upload / small readbacks
+  // the round-4 evaluations: coherent mapped host memory that k_eval_final writes directly
+  plk::PinnedBuf eval_out;
+  void* eval_dev = nullptr;  // eval_out's device address
   plk::DevBuf witness, wires_lag, wires_coef, z_lag, z_coef, num, den, tmp_a, scan_tmp, pi_lag,
-      pi_coef, evq, quotq, t_coef, agg, agg2, w_coef, eval_partial, eval_out, ntt_scratch;
+      pi_coef, evq, quotq, t_coef, agg, agg2, w_coef, eval_partial, ntt_scratch;
   ~plk_prover();
 };
