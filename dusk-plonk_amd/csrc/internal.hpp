@@ -86,6 +86,9 @@ struct plk_domain {
   plk::DevBuf coset_pow;     // g^e, e < n (R' domain)
   plk::DevBuf icoset_scale;  // n^-1 * g^-e, e < n (R' domain)
   std::vector<plk::DevBuf> pass_tw_fwd, pass_tw_inv;  // per pass q > 0: w_{Rp}^{jk} [j][k] (R')
+  // the inverse direction's last pass table times n^-1: a plain idft's scaling rides on the
+  // inter-pass twiddle instead of a product per output (multi-pass plans only)
+  plk::DevBuf pass_tw_inv_last;
   plk::DevBuf scratch;       // 2n elements (default scratch for plk_ntt_dev)
   plk::DevBuf io;            // n elements (host-buffer entry points stage through it)
   std::vector<plk::NttPass> plan;

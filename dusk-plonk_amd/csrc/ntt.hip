@@ -534,6 +534,14 @@ __global__ void k_pass_twiddles(const Fr* __restrict__ tw, Fr* __restrict__ out,
   st_fr(&out[e], ld_fr(&tw[(j * k) << shift]));
 }
 
+// out[e] = in[e] * s (Montgomery product: an R'-domain table times an R-domain scalar stays
+// in the R' domain)
+__global__ void k_scale_table(const Fr* __restrict__ in, Fr* __restrict__ out, Fr s, uint64_t n) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  st_fr(&out[e], fe_mul(ld_fr(&in[e]), s));
+}
+
 // in-place R -> R' domain conversion of a table (ffr.hpp)
 __global__ void k_table_to_rx(const Fr* in, Fr* out, uint64_t n) {
   const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -672,6 +680,11 @@ int ntt_build_domain(plk_domain* d) {
                        d->pass_tw_fwd[q].as<Fr>(), ps.lp, ps.lr, shift);
     hipLaunchKernelGGL(k_pass_twiddles, dim3(pb), dim3(bs), 0, s, d->tw_inv.as<Fr>(),
                        d->pass_tw_inv[q].as<Fr>(), ps.lp, ps.lr, shift);
+    if (q + 1 == d->plan.size()) {  // (R' x R -> R': still an R'-domain table)
+      if ((st = d->pass_tw_inv_last.alloc(cnt * sizeof(Fr)))) return st;
+      hipLaunchKernelGGL(k_scale_table, dim3(pb), dim3(bs), 0, s, d->pass_tw_inv[q].as<Fr>(),
+                         d->pass_tw_inv_last.as<Fr>(), d->n_inv, cnt);
+    }
   }
   PLK_HIP_TRY(hipGetLastError());
   PLK_HIP_TRY(stream_wait(s));
@@ -735,7 +748,10 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
     if (bd > 256) bd = 256;
     const uint32_t blocks = (uint32_t)(n >> (ps.lr + ps.lt));
     const int pre = (first && dir > 0 && coset) ? 1 : 0;
-    const int post = (last && dir < 0) ? (coset ? 2 : 1) : 0;
+    // a plain idft's n^-1 comes with the last pass' inter-pass twiddles (pass_tw_inv_last) when
+    // the plan has more than one pass: one product per element fewer in that pass
+    const bool scaled_tw = last && !first && dir < 0 && !coset;
+    const int post = (last && dir < 0 && !scaled_tw) ? (coset ? 2 : 1) : 0;
     const uint64_t lin = first ? len_in : n;
     // zero-padded input (rows j <= R/8 of the first pass only): closed-form first stages
     const bool prune = first && !last && ps.lr >= 4 &&
@@ -748,7 +764,8 @@ int ntt_run_batch(plk_domain* d, const Fr* in, Fr* out, size_t len_in, int dir, 
                        kL * sizeof(uint32_t);
     dim3 grid(blocks, count);
     const Fr* ptw = q == 0 ? nullptr
-                           : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
+                    : scaled_tw ? d->pass_tw_inv_last.as<Fr>()
+                    : (dir > 0 ? d->pass_tw_fwd[q].as<Fr>() : d->pass_tw_inv[q].as<Fr>());
     NttStrides str;
     str.in = first ? (no_input ? 0 : bt.in_stride) : n * 1;
     str.out = last ? bt.out_stride : n * 1;
