@@ -477,7 +477,8 @@ __global__ void __launch_bounds__(1024) k_sort_small(uint32_t* __restrict__ bloc
 }
 
 // Small batches (B <= kSortSmallMax and at most kSortOneMax scalars per slot: the 2^12-size
-// proofs' commits) sorted by ONE workgroup per slot in ONE dispatch instead of three (k_hist,
+// proofs' commits) sorted in ONE dispatch (round 4: one workgroup per slot; round 5: a few,
+// split by bucket range, below) instead of three (k_hist,
 // k_sort_small, k_scatter) or four (with k_any_nonzero): the commit degree check, an LDS
 // histogram over all of the slot's digits, the scans and task records of k_sort_small, then
 // the scatter with LDS cursors. Small proofs are bound by the command processor's dispatch
@@ -490,6 +491,10 @@ __global__ void __launch_bounds__(1024) k_sort_small(uint32_t* __restrict__ bloc
 // per slot) through one workgroup re-reading the scalars for the scatter: no faster
 // (profiles/r04_sort_one_big_ab.jsonl; removed in round 5).
 constexpr uint32_t kSortOneMax = 8192;  // scalars per slot held in registers
+// workgroups per slot, each taking 1/kSortOneParts of the buckets (round 5, three interleaved
+// runs against one workgroup, profiles/r05_sort_one_parts_ab.jsonl: lone 2^12 MSM 0.394 ->
+// 0.347 ms, 2^12 proofs 8.81 -> 9.10 M, 2^13 within noise; 8 workgroups the same as 4)
+constexpr uint32_t kSortOneParts = 4;
 template <uint32_t C>
 __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, uint64_t n_srs,
                                                    uint32_t chunk, uint32_t* __restrict__ sorted,
@@ -498,9 +503,17 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
                                                    uint32_t* __restrict__ task_off,
                                                    uint2* __restrict__ tasks, uint64_t task_stride,
                                                    uint32_t* __restrict__ flag, uint32_t gen) {
+  // Workgroup x of the slot's gridDim.x owns buckets [bl, bh): every workgroup histograms ALL
+  // the slot's digits (LDS atomics; the offsets of its range follow from the counts below it,
+  // so no workgroup waits for another), then writes the task records and scatters the
+  // entries of its own range only — the scattered 4-byte stores, which one CU's memory path
+  // took most of the kernel's time for, spread over gridDim.x CUs.
   __shared__ uint32_t s_count[kSortSmallMax];
-  __shared__ uint32_t s_c[1024], s_t[1024], s_f[1024], s_len[kChunkMax], s_cur[kChunkMax];
+  __shared__ uint32_t s_c[1024], s_t[1024], s_f[1024], s_len[kChunkMax], s_cur[kChunkMax],
+      s_pre[kChunkMax];
   const uint32_t slot = blockIdx.y, tid = threadIdx.x, nt = 1024, B = cfg.B;  // blockDim.x
+  const uint32_t bpart = B / gridDim.x;  // B and gridDim.x powers of two, B >= gridDim.x
+  const uint32_t bl = blockIdx.x * bpart, bh = bl + bpart;
   const uint32_t len = batch.len[slot];
   const Fr* sc = batch.scalars[slot];
   offsets += (size_t)slot * (B + 1);
@@ -508,10 +521,11 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   tasks += (size_t)slot * task_stride;
   uint32_t* out = sorted + (size_t)slot * sorted_stride;
   // the commit's degree check (k_any_nonzero): a nonzero scalar in [len, check_len)
-  for (uint64_t i = (uint64_t)len + tid; i < batch.check_len[slot]; i += nt)
-    if (!fe_is_zero(ld_fr(&sc[i]))) atomicMax(&flag[slot], gen);
+  if (blockIdx.x == 0)
+    for (uint64_t i = (uint64_t)len + tid; i < batch.check_len[slot]; i += nt)
+      if (!fe_is_zero(ld_fr(&sc[i]))) atomicMax(&flag[slot], gen);
   for (uint32_t b = tid; b < B; b += nt) s_count[b] = 0;
-  for (uint32_t l = tid; l < kChunkMax; l += nt) s_len[l] = 0;
+  for (uint32_t l = tid; l < kChunkMax; l += nt) s_len[l] = s_pre[l] = 0;
   __syncthreads();
   // this thread's scalars (i = tid + k nt, at most kSortOneMax / 1024 of them), brought to
   // [0, (r-1)/2] once and kept in registers for both passes
@@ -535,8 +549,9 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
     hist_digits(sv[k]);
   }
   __syncthreads();
-  // offsets / task offsets / full-task offsets over each thread's contiguous buckets, the
-  // task records (k_sort_small); s_count[b] becomes bucket b's scatter cursor
+  // offsets / task offsets / full-task offsets over each thread's contiguous buckets (all B:
+  // every workgroup derives the same global layout), the tail-length counts over all buckets
+  // and over the buckets below this workgroup's range (its tail ranks start after those)
   const uint32_t per = (B + nt - 1) / nt;
   const uint32_t b0 = min(tid * per, B), b1 = min(b0 + per, B);
   uint32_t c_sum = 0, t_sum = 0, f_sum = 0;
@@ -545,7 +560,10 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
     c_sum += c;
     t_sum += (c + chunk - 1) / chunk;
     f_sum += c / chunk;
-    if (c % chunk) atomicAdd(&s_len[c % chunk], 1u);
+    if (c % chunk) {
+      atomicAdd(&s_len[c % chunk], 1u);
+      if (b < bl) atomicAdd(&s_pre[c % chunk], 1u);
+    }
   }
   s_c[tid] = c_sum;
   s_t[tid] = t_sum;
@@ -560,43 +578,48 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
     s_f[tid] += f;
     __syncthreads();
   }
-  if (tid == 0) {  // tails after the full tasks, longest first
+  if (tid == 0) {  // tails after the full tasks, longest first; this range's after those below
     uint32_t run = s_f[nt - 1];
     for (uint32_t l = chunk - 1; l >= 1; --l) {
-      s_cur[l] = run;
+      s_cur[l] = run + s_pre[l];
       run += s_len[l];
     }
-    offsets[B] = s_c[nt - 1];
-    task_off[B] = s_t[nt - 1];
+    if (blockIdx.x == 0) {
+      offsets[B] = s_c[nt - 1];
+      task_off[B] = s_t[nt - 1];
+    }
   }
   __syncthreads();
   uint32_t c_run = s_c[tid] - c_sum, t_run = s_t[tid] - t_sum, f_run = s_f[tid] - f_sum;
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t cnt = s_count[b];
-    s_count[b] = c_run;
-    offsets[b] = c_run;
-    task_off[b] = t_run;
-    const uint32_t nfull = cnt / chunk, tail = cnt - nfull * chunk;
-    for (uint32_t t = 0; t < nfull; ++t)
-      tasks[f_run + t] = make_uint2(c_run + t * chunk, (t_run + t) | ((chunk - 1) << kTaskShift));
-    if (tail)
-      tasks[atomicAdd(&s_cur[tail], 1u)] =
-          make_uint2(c_run + nfull * chunk, (t_run + nfull) | ((tail - 1) << kTaskShift));
+    if (b >= bl && b < bh) {
+      s_count[b] = c_run;
+      offsets[b] = c_run;
+      task_off[b] = t_run;
+      const uint32_t nfull = cnt / chunk, tail = cnt - nfull * chunk;
+      for (uint32_t t = 0; t < nfull; ++t)
+        tasks[f_run + t] = make_uint2(c_run + t * chunk, (t_run + t) | ((chunk - 1) << kTaskShift));
+      if (tail)
+        tasks[atomicAdd(&s_cur[tail], 1u)] =
+            make_uint2(c_run + nfull * chunk, (t_run + nfull) | ((tail - 1) << kTaskShift));
+    }
     c_run += cnt;
     t_run += (cnt + chunk - 1) / chunk;
-    f_run += nfull;
+    f_run += cnt / chunk;
   }
   __syncthreads();
   auto scatter_digits = [&](const Fr& x, bool neg, uint32_t i) {
     each_digit<C>(x, cfg, [&](uint32_t w, int d) {
-      if (d != 0) {
-        const uint32_t pos = atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
+      const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;  // d = 0: wraps past bh
+      if (b - bl < bpart) {
+        const uint32_t pos = atomicAdd(&s_count[b], 1u);
         out[pos] = (uint32_t)(w * n_srs + i) | (((d < 0) != neg) ? 0x80000000u : 0u);
       }
     });
   };
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter, one workgroup)
+  for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter) of this workgroup's buckets
     const uint32_t i = tid + k * nt;
     if (i >= len) break;
     scatter_digits(sv[k], sneg[k], i);
@@ -1508,7 +1531,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     else PLK_FINE_LAUNCH(8);
 #undef PLK_FINE_LAUNCH
   } else if (sort_one) {
-    PLK_BY_C(s->c, hipLaunchKernelGGL(k_sort_one<CC>, dim3(1, slots), dim3(1024), 0, stream, batch,
+    PLK_BY_C(s->c, hipLaunchKernelGGL(k_sort_one<CC>, dim3(std::min(kSortOneParts, B), slots), dim3(1024), 0, stream, batch,
                                       cfg, (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(),
                                       (uint64_t)w.sorted_stride, w.offsets.as<uint32_t>(),
                                       w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
