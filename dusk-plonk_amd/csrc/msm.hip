@@ -245,15 +245,20 @@ __global__ void k_block_scan(uint32_t* __restrict__ blockhist, uint32_t nblk, ui
 // EXECUTION order of the tasks: all full tasks (CH entries) first in bucket order, then the
 // partial tails grouped by length, longest first, so that a wavefront's lanes run tasks of
 // (nearly) the same length. len_cur[slot][l] = first execution slot of the tails of length l.
-__global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restrict__ counts,
+// The counts are staged in LDS first (dynamic, B words; one coalesced pass): the two walks
+// over each thread's contiguous buckets then read LDS instead of issuing one dependent
+// global load per bucket.
+__global__ void __launch_bounds__(1024) k_scan_buckets(const uint32_t* __restrict__ counts_g,
                                                        uint32_t B, uint32_t chunk,
                                                        uint32_t* __restrict__ offsets,
                                                        uint32_t* __restrict__ task_off,
                                                        uint32_t* __restrict__ full_off,
                                                        uint32_t* __restrict__ len_cur) {
   __shared__ uint32_t s_cnt[1024], s_tsk[1024], s_full[1024], s_len[kChunkMax];
+  extern __shared__ __attribute__((aligned(16))) uint32_t counts[];
   const uint32_t slot = blockIdx.y;
-  counts += (size_t)slot * B;
+  counts_g += (size_t)slot * B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) counts[b] = counts_g[b];
   offsets += (size_t)slot * (B + 1);
   task_off += (size_t)slot * (B + 1);
   full_off += (size_t)slot * B;
@@ -1383,6 +1388,9 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
   if (!w.ev0) PLK_HIP_TRY(hipEventCreate(&w.ev0));
   if (!w.ev1) PLK_HIP_TRY(hipEventCreate(&w.ev1));
   const int lds = (int)(std::min<uint32_t>((uint32_t)B, kLdsBuckets) * 4);
+  if (!wide)  // k_scan_buckets stages the B counts (narrow sets: B <= kLdsBuckets)
+    PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scan_buckets),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   PLK_BY_C(s->c,
            PLK_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hist<CC>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1553,7 +1561,7 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
       hipLaunchKernelGGL(k_block_scan, dim3(cdiv(B, 256), slots), dim3(256), 0, stream,
                          w.blockhist.as<uint32_t>(), hist_blocks, B, w.counts.as<uint32_t>(),
                          (uint32_t*)nullptr, (uint32_t*)nullptr);
-      hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), 0, stream,
+      hipLaunchKernelGGL(k_scan_buckets, dim3(1, slots), dim3(1024), (size_t)B * 4, stream,
                          w.counts.as<uint32_t>(), B, chunk, w.offsets.as<uint32_t>(),
                          w.task_off.as<uint32_t>(), w.full_off.as<uint32_t>(),
                          w.len_cur.as<uint32_t>());

@@ -211,6 +211,8 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_tops(Fr* __restrict__ tot
 // scan of the thread totals in LDS, apply). Small proofs are bound by the rate at which the
 // command processor takes dispatches (~140 k/s with 16 lanes), and the 3-phase
 // form is 3 of them per scan.
+// (round 5: the 3-phase form from n > 4096 instead measured no faster at 2^13-2^15 proofs,
+// profiles/r05_scan_buckets_lds_ab.jsonl)
 constexpr uint32_t kScanSingleThreads = 1024, kScanSingleMax = 32 * kScanSingleThreads;
 // tot[nb] = the grand total, as the 3-phase form leaves it (the grand product's caller reads it)
 template <bool MUL, bool SUFFIX, bool EXCL>
