@@ -528,7 +528,7 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   // the commit's degree check (k_any_nonzero): a nonzero scalar in [len, check_len)
   if (blockIdx.x == 0)
     for (uint64_t i = (uint64_t)len + tid; i < batch.check_len[slot]; i += nt)
-      if (!fe_is_zero(ld_fr(&sc[i]))) atomicMax(&flag[slot], gen);
+      if (!fe_is_zero(ld_fr(&sc[i]))) flag[slot] = gen;  // every writer stores the same value
   for (uint32_t b = tid; b < B; b += nt) s_count[b] = 0;
   for (uint32_t l = tid; l < kChunkMax; l += nt) s_len[l] = s_pre[l] = 0;
   __syncthreads();
@@ -1282,12 +1282,14 @@ __global__ void __launch_bounds__(QUAD ? 512 : 256) k_bitsum2(const G1xyzz* __re
 
 // flag[slot] = gen if any scalar in [len, check_len) is nonzero (commit degree check). The
 // flags are stamped with the batch's generation number instead of being cleared per batch:
-// a stale flag holds an older (smaller) generation, so no memset dispatch is needed.
+// a stale flag holds an older generation, so no memset dispatch is needed. Every writer
+// stores the same value, so a plain store does (no atomic: the flags live in mapped host
+// memory, where an atomic would need the platform's PCIe atomics).
 __global__ void k_any_nonzero(MsmBatch batch, uint32_t* __restrict__ flag, uint32_t gen) {
   const uint32_t slot = blockIdx.y;
   const uint64_t i = (uint64_t)batch.len[slot] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= batch.check_len[slot]) return;
-  if (!fe_is_zero(ld_fr(&batch.scalars[slot][i]))) atomicMax(&flag[slot], gen);
+  if (!fe_is_zero(ld_fr(&batch.scalars[slot][i]))) flag[slot] = gen;
 }
 
 }  // namespace
