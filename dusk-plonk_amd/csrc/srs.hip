@@ -117,13 +117,20 @@ static uint32_t choose_c(size_t n) {
 #define PLK_C_LARGE 17
 #endif
   if (n >= (1u << 16)) return PLK_C_LARGE;
-// 2^14 .. 2^15 points: c = 15 (17 windows, top window 14 bits) against 13 (20 windows):
-// 2^16 bench 18.3 -> 19.4 M constraints/s in round 1 (tools/gpu_ab_c.sh); c = 14 leaves a
-// 2-bit top window (a few huge buckets)
+// 2^15 .. 2^16 points: c = 15 (17 windows of exactly 255 bits); 2^16 bench 18.3 -> 19.4 M
+// constraints/s against 13 in round 1 (tools/gpu_ab_c.sh); round 5 (balanced windows,
+// profiles/r05_window_sizes_ab.jsonl): 2^15 proofs at c = 13 / 14 / 15 20.44 / 20.15 / 20.49 M
 #ifndef PLK_C_MID
 #define PLK_C_MID 15
 #endif
-  if (n >= (1u << 14)) return PLK_C_MID;
+  if (n >= (1u << 15)) return PLK_C_MID;
+  // 2^13 .. 2^15 points (round 5): the short top window that made c = 11-14 lose in round 4
+  // (a few hot buckets) is gone with the balanced windows, and fewer buckets shorten the
+  // reduction tail: 2^14 proofs at c = 13 / 14 / 15 16.86 / 16.71 / 15.70 M (and 17.49 /
+  // 17.20 / 16.16 M on another box), 2^13 at c = 10 / 12 / 13 12.48 / 13.09 / 12.80 M; 2^12
+  // keeps c = 10 (c = 11 / 12 / 13 9.13 / 9.24 / 9.21 against 9.32 M)
+  if (n >= (1u << 14)) return 13;
+  if (n >= (1u << 13)) return 12;
   if (n >= (1u << 10)) return 10;
   return 8;
 }

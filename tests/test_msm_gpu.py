@@ -235,6 +235,40 @@ def test_msm_wide_buckets_vs_oracle(plk, gpu_ctx, oracle, monkeypatch, c, logn):
     assert isinstance(res[-1], plk.PlonkError) and res[-1].status == plk.PLK_E_DEGREE
 
 
+@pytest.mark.parametrize("c,logn", [(11, 12), (12, 13), (13, 12), (13, 14), (14, 14)])
+def test_msm_narrow_balanced_windows_vs_oracle(plk, gpu_ctx, oracle, monkeypatch, c, logn):
+    """Narrow bucket sets with balanced windows (c W - 255 top windows one bit narrower,
+    digits x 2): the window sizes choose_c now takes at 2^13 / 2^14 points (12, 13) and their
+    neighbours, through the one-dispatch sort (<= 8192 scalars) and the k_hist / k_sort_small
+    / k_scatter path (more), with skewed scalar sets and a batch with a degree error."""
+    import torch
+    monkeypatch.setenv("PLK_MSM_C", str(c))
+    n = 1 << logn
+    tau = random_fr(1, seed=800 + c)[0]
+    pp = plk.PlonkParams.setup(logn, tau, gpu_ctx, n_points=n + 8)
+    pts = pp.points()
+    sc = random_fr(n + 8, seed=810 + logn)
+    cases = {
+        "random": sc,
+        "all_same": np.tile(sc[:1], (n + 8, 1)),
+        "sparse": np.where((np.arange(n + 8) % 13 == 0)[:, None], sc, 0).astype(np.uint64),
+        "minus_one": np.tile(fr_int(P.R_MOD - 1), (n + 8, 1)),
+        "high_bits": P.fr_vec_to_np([(1 << 253) + 5 * i for i in range(n + 8)]),
+    }
+    for name, s in cases.items():
+        assert np.array_equal(pp.msm(s).words, oracle.msm(pts, s)), name
+    lens = [n + 3, n // 2, 7]
+    polys = [random_fr(m, seed=820 + i) for i, m in enumerate(lens)]
+    bad = random_fr(n + 20, seed=829)  # longer than the SRS: PLK_E_DEGREE
+    devs = [torch.from_numpy(p.view(np.int64)).cuda() for p in polys + [bad]]
+    torch.cuda.synchronize()
+    res = pp.commit_batch_dev([(d.data_ptr(), d.shape[0]) for d in devs],
+                              torch.cuda.current_stream().cuda_stream, raise_on_error=False)
+    for i, p in enumerate(polys):
+        assert np.array_equal(res[i].words, oracle.msm(pts[: p.shape[0]], p)), i
+    assert isinstance(res[-1], plk.PlonkError) and res[-1].status == plk.PLK_E_DEGREE
+
+
 @pytest.mark.parametrize("tau", [1, P.R_MOD - 1])
 def test_msm_wide_buckets_repeated_points(plk, gpu_ctx, oracle, monkeypatch, tau):
     """Wide bucket sets with tau = +-1 (every SRS point G or -G): equal and opposite points

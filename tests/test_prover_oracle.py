@@ -320,6 +320,30 @@ def test_gpu_proof_equals_oracle_bench_2_16(plk, oracle):
     assert len(pis) == 1 and pis == [fr_int(p) for p in ref["pis"]]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [13, 14])
+def test_gpu_proof_equals_oracle_bench_small(plk, oracle, k):
+    """The bench circuit at the sizes whose commits take c = 12 / 13 (srs.hip choose_c,
+    round 5: balanced windows on the narrow bucket path, k_hist + k_sort_small + k_scatter),
+    GPU proof byte for byte against the restated CPU prover."""
+    import os
+    from dusk_plonk_amd.prover import PlonkKey
+    tau_limbs, _ = tau_for(0x5EED + k)
+    cs = build(bench_chain((1 << k) - 15, 78))
+    gates, wit = cs.export()
+    assert gates.shape[0] == (1 << k) - 8
+    pp = plk.PlonkParams.setup(k, tau_limbs)
+    srs = pp.points(0, n_trim(gates.shape[0]))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    ref = oracle.prove(gates, wit, srs, b"bench", 11, threads)
+    prover, vd = PlonkKey.compile_composer(pp, b"bench", cs)
+    assert np.array_equal(vd.comms, ref["vk"])
+    proof, _ = prover.prove_composer(cs, 11)
+    raw = np.frombuffer(proof.raw_bytes(), dtype=np.uint64)
+    assert np.array_equal(raw[: 11 * 13].reshape(11, 13), ref["comms"])
+    assert np.array_equal(raw[11 * 13:].reshape(16, 4), ref["evals"])
+
+
 GOLD_2_20 = Path(__file__).resolve().parent / "golden" / "proof_2_20.npz"
 
 
