@@ -159,7 +159,9 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
 //   2^15  21.2-21.4 / 20.3-20.9 / 21.3-21.5   -> 0 (2 within noise)
 //   2^17  29.1-29.2 / 28.5-28.5 / 29.0-29.2   -> 0
 //   2^18  29.6-29.8 / 29.0-29.2 / 29.5-29.6   -> 0
-// 2^19 and up as 2^20.
+// 2^19 and up as 2^20. Re-measured after 2^13 / 2^14 moved to c = 12 / 13 (round 5,
+// profiles/r05_tail_forms_new_c_ab.jsonl, three interleaved runs): 2^13 12.71 / 13.17 / 12.74 M
+// -> 1 stays, 2^14 16.87 / 16.18 / 17.37 M -> 2 stays.
 inline int lane_tail_policy(uint64_t n) {
   if (n <= (1ull << 13)) return 1;
   if (n == (1ull << 14)) return 2;
