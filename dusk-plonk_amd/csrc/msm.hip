@@ -85,7 +85,7 @@ __device__ __forceinline__ int digit_at(const Fr& s, uint32_t w, const MsmCfg& c
 }
 
 // Every digit of s, f(w, d) for w = 0 .. W-1 in order. C = 0: digit_at with the run-time
-// window layout. C = the SRS's c (10, 15, 17, 20 — the window sizes choose_c picks): the
+// window layout. C = the SRS's c (10, 12, 13, 15, 17, 20 — the window sizes choose_c picks): the
 // layout is a compile-time constant, the loop unrolls and each digit is a funnel shift
 // (v_alignbit_b32) of two known words, a mask and the carry test — ~6 instructions instead
 // of digit_at's ~25 (word select tree, 64-bit shift). The sort kernels extract every digit of
@@ -500,7 +500,11 @@ constexpr uint32_t kSortOneMax = 8192;  // scalars per slot held in registers
 // runs against one workgroup, profiles/r05_sort_one_parts_ab.jsonl: lone 2^12 MSM 0.394 ->
 // 0.347 ms, 2^12 proofs 8.81 -> 9.10 M, 2^13 within noise; 8 workgroups the same as 4)
 constexpr uint32_t kSortOneParts = 4;
-template <uint32_t C>
+// HOLD: the slot's scalars (<= kSortOneMax) stay in registers between the histogram and the
+// scatter; otherwise (<= kSortOneBig, the 2^14-size commits at c = 13) both passes read them
+// from memory, 4 ahead per thread (for_scalars)
+constexpr uint32_t kSortOneBig = 32768;
+template <uint32_t C, bool HOLD>
 __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, uint64_t n_srs,
                                                    uint32_t chunk, uint32_t* __restrict__ sorted,
                                                    uint64_t sorted_stride,
@@ -532,9 +536,9 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
   for (uint32_t b = tid; b < B; b += nt) s_count[b] = 0;
   for (uint32_t l = tid; l < kChunkMax; l += nt) s_len[l] = s_pre[l] = 0;
   __syncthreads();
-  // this thread's scalars (i = tid + k nt, at most kSortOneMax / 1024 of them), brought to
-  // [0, (r-1)/2] once and kept in registers for both passes
-  constexpr uint32_t kPer = kSortOneMax / 1024;
+  // HOLD: this thread's scalars (i = tid + k nt, at most kSortOneMax / 1024 of them), brought
+  // to [0, (r-1)/2] once and kept in registers for both passes
+  constexpr uint32_t kPer = HOLD ? kSortOneMax / 1024 : 1;
   Fr sv[kPer];
   bool sneg[kPer];
   auto hist_digits = [&](const Fr& x) {
@@ -542,16 +546,20 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
       if (d != 0) atomicAdd(&s_count[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
     });
   };
+  if constexpr (HOLD) {
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t i = tid + k * nt;
-    sneg[k] = false;
-    if (i < len) sv[k] = scalar_half(&sc[i], sneg[k]);
-  }
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * nt;
+      sneg[k] = false;
+      if (i < len) sv[k] = scalar_half(&sc[i], sneg[k]);
+    }
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {  // histogram of every digit of the slot
-    if (tid + k * nt >= len) break;
-    hist_digits(sv[k]);
+    for (uint32_t k = 0; k < kPer; ++k) {  // histogram of every digit of the slot
+      if (tid + k * nt >= len) break;
+      hist_digits(sv[k]);
+    }
+  } else {
+    for_scalars(sc, 0, len, tid, nt, [&](uint32_t, const Fr& x, bool) { hist_digits(x); });
   }
   __syncthreads();
   // offsets / task offsets / full-task offsets over each thread's contiguous buckets (all B:
@@ -623,11 +631,16 @@ __global__ void __launch_bounds__(1024) k_sort_one(MsmBatch batch, MsmCfg cfg, u
       }
     });
   };
+  if constexpr (HOLD) {
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter) of this workgroup's buckets
-    const uint32_t i = tid + k * nt;
-    if (i >= len) break;
-    scatter_digits(sv[k], sneg[k], i);
+    for (uint32_t k = 0; k < kPer; ++k) {  // scatter (k_scatter) of this workgroup's buckets
+      const uint32_t i = tid + k * nt;
+      if (i >= len) break;
+      scatter_digits(sv[k], sneg[k], i);
+    }
+  } else {
+    for_scalars(sc, 0, len, tid, nt,
+                [&](uint32_t i, const Fr& x, bool neg) { scatter_digits(x, neg, i); });
   }
 }
 
@@ -1318,6 +1331,8 @@ static G1xyzz rx_to_r_domain(const G1xyzz& p) {
 #define PLK_BY_C(c_, ...)                          \
   switch (c_) {                                    \
     case 10: { constexpr uint32_t CC = 10; __VA_ARGS__; } break; \
+    case 12: { constexpr uint32_t CC = 12; __VA_ARGS__; } break; \
+    case 13: { constexpr uint32_t CC = 13; __VA_ARGS__; } break; \
     case 15: { constexpr uint32_t CC = 15; __VA_ARGS__; } break; \
     case 17: { constexpr uint32_t CC = 17; __VA_ARGS__; } break; \
     case 20: { constexpr uint32_t CC = 20; __VA_ARGS__; } break; \
@@ -1499,7 +1514,13 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
   }
   const uint32_t gen = w.gen;
   // small batches: the whole sort (and the degree check) in one dispatch per batch
-  const bool sort_one = small_batch;
+  // (the chunk floor stays small_batch's: more scalars than kSortOneMax keep kChunkMin tasks).
+  // Round 5: up to kSortOneBig scalars too (the 2^14-size commits at c = 13) instead of
+  // k_hist + k_sort_small + k_scatter: 2^14 proofs 16.77 -> 17.33 M, 2^13 / 2^12 within noise
+  // (profiles/r05_sort_one_big_c13_ab.jsonl; round 4's single-workgroup form at c = 15 did
+  // not pay, profiles/r04_sort_one_big_ab.jsonl)
+  const bool sort_one = small_batch || (!wide && B <= kSortSmallMax && max_len <= kSortOneBig);
+  const bool hold = max_len <= kSortOneMax;
   if (max_tail && !sort_one) {
     hipLaunchKernelGGL(k_any_nonzero, dim3(cdiv(max_tail, 256), slots), dim3(256), 0, stream,
                        batch, hdr_dev->flag, gen);
@@ -1541,11 +1562,18 @@ int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const
     else PLK_FINE_LAUNCH(8);
 #undef PLK_FINE_LAUNCH
   } else if (sort_one) {
-    PLK_BY_C(s->c, hipLaunchKernelGGL(k_sort_one<CC>, dim3(std::min(kSortOneParts, B), slots), dim3(1024), 0, stream, batch,
-                                      cfg, (uint64_t)s->n, chunk, w.sorted.as<uint32_t>(),
-                                      (uint64_t)w.sorted_stride, w.offsets.as<uint32_t>(),
-                                      w.task_off.as<uint32_t>(), w.tasks.as<uint2>(),
-                                      (uint64_t)w.task_stride, hdr_dev->flag, gen))
+#define PLK_SORT_ONE_LAUNCH(HOLD)                                                                  \
+  PLK_BY_C(s->c, hipLaunchKernelGGL((k_sort_one<CC, HOLD>), dim3(std::min(kSortOneParts, B), slots), \
+                                    dim3(1024), 0, stream, batch, cfg, (uint64_t)s->n, chunk,        \
+                                    w.sorted.as<uint32_t>(), (uint64_t)w.sorted_stride,              \
+                                    w.offsets.as<uint32_t>(), w.task_off.as<uint32_t>(),             \
+                                    w.tasks.as<uint2>(), (uint64_t)w.task_stride, hdr_dev->flag, gen))
+    if (hold) {
+      PLK_SORT_ONE_LAUNCH(true);
+    } else {
+      PLK_SORT_ONE_LAUNCH(false);
+    }
+#undef PLK_SORT_ONE_LAUNCH
   } else {
     const size_t lds = (size_t)std::min<uint32_t>(B, kLdsBuckets) * 4;
     if (max_len) {
