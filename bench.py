@@ -568,6 +568,18 @@ def host_info():
     return {"nproc": os.cpu_count(), "usable_cores": usable, "cpu_model": model}
 
 
+def stored_clock(form_name: str):
+    """The stored DVFS reading of a k_accumulate form (profiles/r05_effective_clock.json: the
+    effective shader clock from GRBM_GUI_ACTIVE and the VALU activity per wave from the SQ
+    counters, one --pmc pass each, tools/gpu_r05_y.sh), or None."""
+    f = Path(__file__).resolve().parent / "profiles" / "r05_effective_clock.json"
+    try:
+        d = json.loads(f.read_text()).get(form_name)
+    except (OSError, ValueError):
+        return None
+    return d if isinstance(d, dict) and d.get("effective_ghz") else None
+
+
 def valu_roofline(adds_per_s, form=ACC_LANE):
     """k_accumulate against its binding ceiling, VALU issue: each mixed addition's compiled
     instruction mix (of the instantiation that ran: `form`) priced at the measured
@@ -577,7 +589,18 @@ def valu_roofline(adds_per_s, form=ACC_LANE):
     isa = compiled_loop(form[0])
     achieved = adds_per_s / 64.0 * isa["valu_cycles"]
     mads = adds_per_s * isa["v_mad_u64_u32"]
-    return {"bound": "valu", "achieved": achieved, "peak": SIMD_CYCLES_PEAK,
+    clk = stored_clock(form[1])
+    dvfs = None
+    if clk:  # the clock the chip holds under this kernel, and how busy its VALU is there
+        ghz = clk["effective_ghz"]
+        # (no frac against that clock: it was read in a profiled pass, which runs a few % below
+        # the un-profiled clock of this line, MI355X_MICROARCH.md)
+        dvfs = {"effective_clock_ghz": ghz,
+                "valu_busy_per_simd": (clk["valu_per_wave"] or 0.0) * clk["waves_per_simd"],
+                "source": "stored profiles/r05_effective_clock.json (" + clk["run"] + "): clock = "
+                          "GRBM_GUI_ACTIVE / 8 XCDs / dispatch time, VALU busy per SIMD = "
+                          "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES x waves per SIMD"}
+    return {"bound": "valu", "achieved": achieved, "peak": SIMD_CYCLES_PEAK, "dvfs": dvfs,
             "unit": "SIMD issue-cycles/s", "frac": achieved / SIMD_CYCLES_PEAK,
             "peak_source": "1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md); per-instruction issue "
                            "costs measured by tools/ubench_issue.hip (profiles/r03_ubench_issue.txt)",
@@ -603,7 +626,8 @@ def binding_roofline(valu: dict, hbm_achieved_gbs: float, alg_bytes: float, traf
             "instructions_per_point_add": valu["instructions_per_point_add"],
             "valu_instructions_per_point_add": valu.get("valu_instructions_per_point_add"),
             "s_nop_per_point_add": valu.get("s_nop_per_point_add"),
-            "mads_source": valu["mads_source"], "mad": valu["mad"], "traffic": traffic,
+            "mads_source": valu["mads_source"], "mad": valu["mad"], "dvfs": valu.get("dvfs"),
+            "traffic": traffic,
             "hbm": {"achieved": hbm_achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm_achieved_gbs / HBM_PEAK_GBS,
                     "algorithmic_bytes_per_launch": alg_bytes,

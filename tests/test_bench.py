@@ -90,6 +90,21 @@ def test_compiled_loop_mads():
     assert lane["valu_instructions"] < lone["valu_instructions"]
 
 
+def test_valu_roofline_carries_stored_clock():
+    """The VALU roofline of each k_accumulate form carries the stored DVFS reading
+    (profiles/r05_effective_clock.json: effective clock from GRBM_GUI_ACTIVE, VALU busy per
+    SIMD from the SQ counters): the top-level frac is priced at the nominal 2.4 GHz."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    for form in (bench.ACC_LANE, bench.ACC_LONE):
+        r = bench.valu_roofline(7.0e9, form)
+        d = r["dvfs"]
+        assert d is not None, form
+        assert 1.0 < d["effective_clock_ghz"] < 2.5
+        assert 0.5 < d["valu_busy_per_simd"] < 1.2
+        assert "r05_effective_clock.json" in d["source"]
+
+
 def test_gpus_flag_must_match_launcher():
     """Under a launcher (WORLD_SIZE set) --gpus must agree with it: no silent n_gpus: 1."""
     env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
