@@ -596,10 +596,13 @@ def valu_roofline(adds_per_s, form=ACC_LANE):
         # (no frac against that clock: it was read in a profiled pass, which runs a few % below
         # the un-profiled clock of this line, MI355X_MICROARCH.md)
         dvfs = {"effective_clock_ghz": ghz,
-                "valu_busy_per_simd": (clk["valu_per_wave"] or 0.0) * clk["waves_per_simd"],
+                "sq_valu_active_per_wave": clk["valu_per_wave"],
+                "waves_per_simd": clk["waves_per_simd"],
                 "source": "stored profiles/r05_effective_clock.json (" + clk["run"] + "): clock = "
-                          "GRBM_GUI_ACTIVE / 8 XCDs / dispatch time, VALU busy per SIMD = "
-                          "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES x waves per SIMD"}
+                          "GRBM_GUI_ACTIVE / 8 XCDs / dispatch time; SQ_ACTIVE_INST_VALU / "
+                          "SQ_WAVE_CYCLES per wave (its product with the waves per SIMD is ~1.0 "
+                          "here, but reads 1.3 for the NTT pass at 4 waves: the counter's active "
+                          "cycles overlap across waves, so it bounds the VALU busy fraction from above)"}
     return {"bound": "valu", "achieved": achieved, "peak": SIMD_CYCLES_PEAK, "dvfs": dvfs,
             "unit": "SIMD issue-cycles/s", "frac": achieved / SIMD_CYCLES_PEAK,
             "peak_source": "1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md); per-instruction issue "
