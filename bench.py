@@ -130,6 +130,10 @@ def parse():
                     help="--mode msm --shard-msm: by bucket range (each rank sorts, accumulates "
                          "and reduces 1/G of the buckets; plk_commit_batch_dev_part) or by SRS "
                          "slice (each rank the whole Pippenger over 1/G of the points)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="prove mode: skip the extra measurements attached to the line after the "
+                         "timed region (n_2_16: the metric's second size; msm_shard: one 2^k MSM "
+                         "split over all ranks by bucket range, the north star's MSM scaling curve)")
     ap.add_argument("--bucket-parts", type=int, default=1,
                     help="--mode msm on ONE GPU: run the MSM as P bucket-range parts one after "
                          "the other (what each of P GPUs would run under --shard-msm), timing "
@@ -422,7 +426,8 @@ def cpu_concurrent(gates, wit, srs, vk, procs: int, n: int) -> dict:
             "window_value": procs * n / window, "window_s": window}
 
 
-def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=None):
+def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=None,
+                      gpu_value_16=None):
     """Restated reference CPU prover (oracle/plk_prover_oracle.c: key compile + create_proof
     in the reference's order and cost structure, OpenMP where the reference uses rayon,
     sequential where it is sequential — notably the quotient loop's one v_h inversion per 8n
@@ -491,6 +496,13 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=No
             node20 = None
     out = {
         "value": conc["value"], "unit": "constraints/s", "cores": conc["procs"], "kind": "port",
+        "value_log_n": ks,
+        "value_note": (f"`value` is measured in this run at n=2^{ks}" + (
+            f", not at the line's 2^{k}: {conc['procs']} concurrent 2^{k} proofs take ~5 minutes "
+            "(too long for every run); the stored 2^20 measurement of the same kind is "
+            "`concurrent_2_20` (ratio `gpu_over_measured_2_20_share`), and `gpu_16_over_cpu_16` "
+            "compares the line's own 2^16 figure (n_2_16) with `value` at the same size"
+            if ks != k else "")),
         "measure": (f"MEASURED throughput of {conc['procs']} concurrent independent proofs at "
                     f"n=2^{ks} (one process and thread each, every core of this process's "
                     "share); an upper bound of the CPU's 2^20 throughput"),
@@ -525,6 +537,8 @@ def cpu_baseline_full(k: int, pp, threads: int, k_sample: int = 16, gpu_value=No
                         "gpu_over_latency": gpu_value / out["latency"]["value"]}
         if node20:
             out["ratio"]["gpu_over_measured_2_20_share"] = gpu_value / node20["value"]
+        if gpu_value_16:
+            out["ratio"]["gpu_16_over_cpu_16"] = gpu_value_16 / conc["value"]
     return out
 
 
@@ -690,6 +704,130 @@ def acc_roofline(ms_total, launches, adds, points, label, form=ACC_LANE):
             "point_adds_per_launch": adds / launches,
             "point_adds_per_s": adds / (ms_total * 1e-3),
             "valu": valu_roofline(adds / (ms_total * 1e-3), form), "timing": label}
+
+
+def msm_shard_point(plk, torch, dist, world, rank, device, pp, k, steps, warmup, threads):
+    """One point of the north star's MSM scaling curve per driver run: ONE 2^k MSM
+    per step (uniform scalars, the same on every rank, resident in HBM; the bench SRS), split
+    over ALL ranks by bucket range (plk_commit_batch_dev_part: rank r sorts, accumulates and
+    reduces 1/G of the 2^(c-1) buckets of the whole MSM) with one all-gather of one point per
+    rank and the host fold (parallel.gather_fold); at world 1 the lone MSM (the curve's N = 1
+    point). Every rank holds the whole SRS (the proof batches' own), so each checks the fold
+    against the unsplit commit of the same scalars; world 1 checks against the oracle."""
+    from dusk_plonk_amd.parallel import bucket_parts_ok, gather_fold
+    n = 1 << k
+    gpu = torch.cuda.is_available()  # (False only in the CPU test of this function's logic)
+    s = torch.cuda.current_stream().cuda_stream if gpu else 0
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
+    x = rand_fr_dev(torch, n, 4343, device)
+    split = world > 1 and bucket_parts_ok(pp.n, world)
+    comm_dev = device if dist.get_backend() == "nccl" else None
+    coms, part_s = [], []
+
+    def one(timed):
+        t0 = time.perf_counter()
+        if split:
+            part = pp.commit_batch_dev([(x.data_ptr(), n)], s, part=rank, parts=world)
+            t1 = time.perf_counter()
+            w = np.zeros((1, 13), dtype=np.uint64)
+            w[0] = part[0].words
+            com = gather_fold(w, [0], None, comm_dev)[0]
+        else:
+            com = pp.commit_dev(x.data_ptr(), n, s)
+            t1 = time.perf_counter()
+        if timed:
+            coms.append(com)
+            part_s.append(t1 - t0)
+
+    for _ in range(warmup):
+        one(False)
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one(True)
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(torch, dist, elapsed, device)
+    want = pp.commit_dev(x.data_ptr(), n, s)  # unsplit, on this rank's whole SRS
+    ok = all(c == want for c in coms)
+    check = "every rank: the fold against its own unsplit commit of the same scalars"
+    if world == 1:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_lib
+        orc = oracle_lib.load()
+        ok = ok and np.array_equal(orc.msm(pp.points(0, n), x.cpu().numpy().view(np.uint64), threads),
+                                   want.words)
+        check = f"against the oracle's Pippenger (oracle/plk_oracle.c, {threads} threads)"
+    mine = {"rank": rank, "part_ms": 1e3 * float(np.mean(part_s)), "ok": bool(ok)}
+    allr = [mine]
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+    return {"n": n, "parts": world if split else 1,
+            "split": ("bucket range" if split else
+                      "none (lone MSM: the curve's N = 1 point)" if world == 1 else
+                      f"none ({world} bucket ranges not valid for this SRS)"),
+            "transport": transport(dist) if split else None,
+            "ms_per_msm": elapsed * 1e3 / steps, "msm_per_s": steps / elapsed, "steps": steps,
+            "points_per_s": n * steps / elapsed,
+            "per_rank_part_ms": [r["part_ms"] for r in allr],
+            "bit_exact": all(r["ok"] for r in allr), "check": check,
+            "note": "strong scaling of ONE MSM over the ranks (the north star's 8-GPU MSM curve); "
+                    "part_ms = a rank's own part, host-timed launch to readback; ms_per_msm includes "
+                    "the all-gather and the fold, max over ranks"}
+
+
+def run_second_size(args, plk, torch, dist, world, rank, device, k2: int):
+    """The metric's second size (BASELINE: 'at n=2^16 and 2^20'): a short prove run at 2^k2
+    with the default lanes for that size, proof batches on every rank (key and SRS built
+    outside the timed region, fresh witnesses), every lane's last proof re-proved alone and
+    byte-compared (proofs_checked)."""
+    n2 = 1 << k2
+    L = 12 if k2 >= 18 else 14 if k2 >= 15 else 16
+    ctx = plk.Context.default(torch.cuda.current_device())
+    base = ProverBase(plk, k2, ctx)
+    lanes = [ProofLane(base, 1000 * rank + 23 + 101 * l) for l in range(L)]
+    import concurrent.futures as cf
+    drivers = cf.ThreadPoolExecutor(L)
+
+    def run(count, which=None):
+        for f in [drivers.submit(lambda ln: [ln.step() for _ in range(count)], ln)
+                  for ln in (which or lanes)]:
+            f.result()
+
+    run(max(1, min(args.warmup, 3)))
+    torch.cuda.synchronize()
+    steps = args.steps
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(torch, dist, elapsed, device)
+    checked, bad = recheck_proofs(lanes, lanes[0])
+    for ln in lanes:
+        ln.pool.shutdown(wait=True)
+        ln.lane.close()
+    drivers.shutdown()
+    if bad:
+        raise SystemExit(f"bench.py: 2^{k2}: {len(bad)} of {checked} concurrent proofs differ "
+                         f"from the same proof made alone (seeds {bad})")
+    return {"value": n2 * steps * L * world / elapsed, "unit": "constraints/s", "log_n": k2,
+            "ms_per_step": elapsed * 1e3 / steps, "steps": steps, "lanes": L,
+            "proofs_per_step": L * world, "proofs_checked": checked - len(bad),
+            "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+            "note": f"same workload as the headline at n=2^{k2} (m = {base.gates} gates, 1 public "
+                    "input), timed after it in the same process; HIP hardware queues as sized "
+                    "for the headline's lanes"}
 
 
 def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
@@ -862,23 +1000,50 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
         dist.all_gather_object(allr, mine)
         r["per_rank"] = allr
         r["note"] += "; per_rank: every rank's own solo figures (top level: rank 0's)"
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_full(k, base.pp, cpu_threads(args),
-                                                   gpu_value=result["value"])
-    elif rank == 0 and world > 1:
-        result["cpu_baseline"] = stored_cpu_baseline(k, world, result["value"])
-    if rank == 0:
-        print(json.dumps(result), flush=True)
     for ln in lanes_all:
         ln.pool.shutdown(wait=True)
         ln.lane.close()
     if exchange is not None:
         exchange.close()
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    drivers.shutdown()
     if mismatched:
+        if rank == 0:
+            emit(result)
         raise SystemExit(f"bench.py: {len(mismatched)} of {checked} concurrent proofs differ "
                          f"from the same proof made alone (seeds {mismatched})")
+    if not args.no_extras and not shard:
+        # after the timed region: the north star's MSM curve point (one 2^k MSM over all ranks)
+        # and the metric's second size
+        result["msm_shard"] = msm_shard_point(plk, torch, dist, world, rank, device, base.pp, k,
+                                              args.steps, max(1, min(args.warmup, 3)),
+                                              cpu_threads(args))
+        if not result["msm_shard"]["bit_exact"]:
+            if rank == 0:
+                emit(result)
+            raise SystemExit("bench.py: the split MSM differs from the unsplit commit")
+        if k != 16:
+            result["n_2_16"] = run_second_size(args, plk, torch, dist, world, rank, device, 16)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_full(
+            k, base.pp, cpu_threads(args), gpu_value=result["value"],
+            gpu_value_16=(result.get("n_2_16") or {}).get("value") if k != 16 else result["value"])
+    elif rank == 0 and world > 1:
+        result["cpu_baseline"] = stored_cpu_baseline(k, world, result["value"])
+    if rank == 0:
+        emit(result)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+BUILD_INFO: dict = {}
+
+
+def emit(result: dict):
+    """Print the line (rank 0), stamped with the library's build provenance (plk_build_info:
+    hashes of the sources and flags it was compiled from, checked against this tree)."""
+    if BUILD_INFO:
+        result["build_id"] = {k: BUILD_INFO.get(k) for k in ("src", "flags", "variant", "tree_src")}
+    print(json.dumps(result), flush=True)
 
 
 def transport(dist) -> str:
@@ -925,12 +1090,18 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
             comm_dev = device if dist.get_backend() == "nccl" else None
 
             def step(timed):
-                t0 = time.perf_counter()
-                part = pp.commit_batch_dev([(x.data_ptr(), n)], s, raise_on_error=False,
-                                           **({"part": rank, "parts": world}
-                                              if spp.mode == "buckets" else {}))
-                t1 = time.perf_counter()
                 from dusk_plonk_amd.parallel import gather_fold
+                t0 = time.perf_counter()
+                if spp.mode == "buckets":  # this rank's bucket range of the whole MSM
+                    part = pp.commit_batch_dev([(x.data_ptr(), n)], s, raise_on_error=False,
+                                               part=rank, parts=world)
+                else:  # this rank's SRS slice: its span of the scalars against its points
+                    off, m = spp._local_spans(n)
+                    part = pp.commit_batch_dev([(x.data_ptr() + 32 * off, m)], s,
+                                               raise_on_error=False)
+                t1 = time.perf_counter()
+                if isinstance(part[0], plk.PlonkError):
+                    raise part[0]
                 w = np.zeros((1, 13), dtype=np.uint64)
                 w[0] = part[0].words
                 coms.append(gather_fold(w, [0], None, comm_dev)[0])
@@ -1053,6 +1224,20 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
                                    f"replicas x{world}")},
         "roofline": roof,
     }
+    if args.mode == "msm" and args.shard_msm and world > 1:
+        # the folded commitment against an unsplit commit of the same scalars on a whole SRS
+        # (buckets: every rank's own; points: one built for the check), on every rank
+        full = spp.local if spp.mode == "buckets" else plk.PlonkParams.setup(k, tau, ctx)
+        want = full.commit_dev(x.data_ptr(), n, s)
+        ok = all(c == want for c in coms)
+        on = device if dist.get_backend() == "nccl" else "cpu"
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=on)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        result["bit_exact_vs_unsplit"] = bool(flag.item())
+        if not result["bit_exact_vs_unsplit"]:
+            if rank == 0:
+                emit(result)
+            raise SystemExit("bench.py: the split MSM's fold differs from the unsplit commit")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = cpu_threads(args)
         sys.path.insert(0, str(ROOT / "tests"))
@@ -1082,10 +1267,10 @@ def run_kernel_mode(args, plk, torch, dist, world, rank, device, k, n):
         result["cpu_baseline"] = {"value": units / cpu_s, "unit": "points/s", "cores": threads,
                                   "kind": "port", "host": host_info(), "sample": sample}
         if not exact:
-            print(json.dumps(result), flush=True)
+            emit(result)
             raise SystemExit("GPU result differs from the oracle")
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -1150,6 +1335,9 @@ def main():
 
     import dusk_plonk_amd as plk
 
+    # the library must come from this tree's sources (fails loudly otherwise); the line
+    # carries the ids
+    BUILD_INFO.update(plk.check_build())
     k = args.log_n
     n = 1 << k
     # An explicit stream: torch's default stream has handle 0, which the ABI maps to the
@@ -1251,7 +1439,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(k, hp.pp, cpu_threads(args))
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -6,11 +6,11 @@ in include/plk.h. See DESIGN.md.
 """
 from .plonk import (  # noqa: F401
     ABI_SYMBOLS, Coefficients, Commitment, Context, Fft, PLK_E_ARG, PLK_E_DEGREE, PLK_E_DEVICE,
-    PLK_E_NODEV, PLK_E_OOM, PLK_OK, PlonkError, PlonkParams, PointsValue, device_count, g1_sum,
-    msm_sharded,
+    PLK_E_NODEV, PLK_E_OOM, PLK_OK, PlonkError, PlonkParams, PointsValue, build_info, check_build,
+    device_count, g1_sum, msm_sharded,
 )
 
 __all__ = [
     "ABI_SYMBOLS", "Coefficients", "Commitment", "Context", "Fft", "PlonkError", "PlonkParams",
-    "PointsValue", "device_count", "g1_sum", "msm_sharded",
+    "PointsValue", "build_info", "check_build", "device_count", "g1_sum", "msm_sharded",
 ]

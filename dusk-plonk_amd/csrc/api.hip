@@ -80,11 +80,6 @@ int plk_ctx_create(int device, plk_ctx** out) {
   DeviceGuard g(device);
   std::unique_ptr<plk_ctx> c(new plk_ctx());
   c->device = device;
-  {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
-      c->cus = cus;
-  }
   PLK_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   *out = c.release();
   return PLK_OK;

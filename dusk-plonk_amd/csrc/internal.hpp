@@ -139,7 +139,6 @@ struct plk_srs {
 
 struct plk_ctx {
   int device = 0;
-  int cus = 256;  // compute units (hipDeviceAttributeMultiprocessorCount)
   hipStream_t stream = nullptr;
   std::map<uint32_t, std::unique_ptr<plk_domain>> domains;
   std::mutex mu;

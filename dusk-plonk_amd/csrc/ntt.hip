@@ -352,7 +352,7 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
       if (PRE == 1) aux[c] = ld_fr(&pre[gc]);
     }
     // inter-pass twiddle w_{Rp}^{jk} from the pass table laid out [j][k] (coalesced in k);
-    // every (j, k) is in the table, the j = 0 / k = 0 entries are skipped below
+    // every (j, k) is in the table and every entry is multiplied below (see there)
     if (PRE != 1 && lp != 0) {
 #pragma unroll
       for (uint32_t c = 0; c < kLoadIt; ++c) {
@@ -412,8 +412,10 @@ __global__ void __launch_bounds__(256, PLK_NTT_MINW) k_ntt_pass(const Fr* __rest
         v = rx_unpack(raw[c]);
         if (PRE == 1) v = rx_mul(v, rx_unpack(aux[c]));
       }
-      // inter-pass twiddle: unconditional (the j = 0 / k = 0 entries are one; a wave's lanes
-      // all multiply anyway, and the lane-dependent skip cost registers)
+      // inter-pass twiddle: the multiply MUST stay unconditional. A plain idft's last pass
+      // reads pass_tw_inv_last, whose entries carry n^-1 (round 5: the idft scaling rides on
+      // this table), so its j = 0 / k = 0 entries are n^-1, not one; skipping the "identity"
+      // entries would drop the scaling on those rows (test_idft_multipass_identity_rows)
       if (PRE != 1 && lp != 0) v = rx_mul(v, rx_unpack(aux[c]));
       return v;
     };

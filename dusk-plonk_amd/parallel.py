@@ -311,18 +311,34 @@ def shard_prover_lane(lane, tau, n_points: int, group=None, device=None, ctx=Non
 
 
 def window_bits(n_points: int) -> int:
-    """The MSM window size c the library picks for an SRS of n_points (srs.hip choose_c,
-    without the PLK_MSM_C override)."""
-    return 20 if n_points >= 1 << 20 else 17 if n_points >= 1 << 16 else 15 if n_points >= 1 << 14 else 0
+    """The MSM window size c an SRS of n_points runs with: srs.hip choose_c (including its
+    PLK_MSM_C override, which accepts 8..22 except 21) and msm_prepare_srs's mapping of a c
+    whose every window would be c - 1 bits wide (c = 18) to c - 1 (oracle/pyref.py
+    msm_effective_c)."""
+    import os
+    c = 0
+    env = os.environ.get("PLK_MSM_C")
+    if env:
+        try:
+            v = int(env)
+        except ValueError:
+            v = 0
+        if 8 <= v <= 22 and v != 21:
+            c = v
+    if not c:
+        c = (20 if n_points >= 1 << 20 else 17 if n_points >= 1 << 16 else
+             15 if n_points >= 1 << 15 else 13 if n_points >= 1 << 14 else
+             12 if n_points >= 1 << 13 else 10 if n_points >= 1 << 10 else 8)
+    return c - 1 if (c - 1) * ((255 + c - 1) // c) == 255 else c
 
 
 def bucket_parts_ok(n_points: int, parts: int) -> bool:
-    """Whether plk_commit_batch_dev_part accepts `parts` bucket ranges on an SRS of n_points:
-    a power of two, a wide bucket set (c >= 17) and >= 2^14 buckets per part."""
-    import os
-    c = int(os.environ.get("PLK_MSM_C", "0")) or window_bits(n_points)
-    return (parts >= 1 and parts & (parts - 1) == 0 and c >= 17
-            and (1 << (c - 1)) // parts >= 1 << 14)
+    """Whether plk_commit_batch_dev_part accepts `parts` bucket ranges on an SRS of n_points
+    (msm.hip msm_commit_batch_part): a power of two, a wide bucket set (2^(c-1) above the
+    32 K LDS buckets, c >= 17) and >= 2^14 buckets per part."""
+    c = window_bits(n_points)
+    return (parts >= 1 and parts & (parts - 1) == 0
+            and (parts == 1 or (c >= 17 and (1 << (c - 1)) // parts >= 1 << 14)))
 
 
 class ShardedPlonkParams:

@@ -34,7 +34,7 @@ PLK_OK, PLK_E_DEGREE, PLK_E_ARG, PLK_E_DEVICE, PLK_E_OOM, PLK_E_NODEV = range(6)
 
 # Symbols declared in include/plk.h (checked by tests/test_abi.py)
 ABI_SYMBOLS = (
-    "plk_abi_version", "plk_status_str", "plk_device_count", "plk_ctx_create",
+    "plk_abi_version", "plk_status_str", "plk_build_info", "plk_device_count", "plk_ctx_create",
     "plk_ctx_destroy", "plk_ctx_stream", "plk_ctx_synchronize", "plk_domain_get",
     "plk_domain_info", "plk_domain_elements", "plk_domain_vanishing_over_coset", "plk_ntt",
     "plk_ntt_dev", "plk_ntt_batch_dev", "plk_srs_setup", "plk_srs_load", "plk_srs_destroy",
@@ -88,6 +88,7 @@ def _lib():
         sig = {
             "plk_abi_version": (i32, []),
             "plk_status_str": (C.c_char_p, [i32]),
+            "plk_build_info": (C.c_char_p, []),
             "plk_device_count": (i32, [C.POINTER(i32)]),
             "plk_ctx_create": (i32, [i32, pp]),
             "plk_ctx_destroy": (i32, [vp]),
@@ -128,6 +129,38 @@ def _lib():
             f.restype, f.argtypes = res, args
         _LIB = lib
     return _LIB
+
+
+def build_info() -> dict:
+    """plk_build_info of the loaded library: {'src', 'flags', 'variant', 'lib'}."""
+    raw = _lib().plk_build_info().decode()
+    d = dict(kv.split("=", 1) for kv in raw.split())
+    d["lib"] = str(_LIB_PATH)
+    return d
+
+
+def check_build(root: Path | None = None) -> dict:
+    """Refuse a library built from other sources than the tree it is loaded from (round-5
+    verdict: a pushed prebuilt libplk.so was not tied to its sources). The default library
+    must also carry the default flags; a PLK_LIB variant (tools/ab.py) may differ in flags.
+    Returns build_info() with the tree's ids; raises ImportError on a mismatch."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_plk_build_ext", _PKG / "build_ext.py")
+    be = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(be)
+    info = build_info()
+    tree_src = be.source_id(root or be.ROOT)
+    info["tree_src"] = tree_src
+    if os.environ.get("PLK_LIB") and os.environ.get("PLK_LIB_ANY_SRC") == "1":
+        info["src_check"] = "skipped (PLK_LIB variant with PLK_LIB_ANY_SRC=1: an A/B against another tree)"
+        return info
+    if info.get("src") != tree_src:
+        raise ImportError(f"{_LIB_PATH} was built from other sources (library src={info.get('src')}, "
+                          f"tree src={tree_src}): rebuild with __graft_entry__.build()")
+    if not os.environ.get("PLK_LIB") and info.get("flags") != be.flags_id():
+        raise ImportError(f"{_LIB_PATH} was built with other flags (library flags={info.get('flags')}, "
+                          f"default flags={be.flags_id()}): rebuild with __graft_entry__.build()")
+    return info
 
 
 def _check(status: int, what: str):

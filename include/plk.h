@@ -56,6 +56,11 @@ typedef struct plk_key plk_key;
 /* ---- library / context ------------------------------------------------------------- */
 int plk_abi_version(void);
 const char* plk_status_str(int status);
+/* Build provenance (no reference counterpart): "src=<16 hex> flags=<16 hex> variant=<name>",
+ * src = a hash of csrc/ *.hip, csrc/ *.hpp and this header as they were compiled, flags = a hash
+ * of the hipcc flags (build_ext.py source_id / flags_id). The Python mirror refuses a library
+ * whose src differs from the tree it is loaded from (plonk.check_build). */
+const char* plk_build_info(void);
 /* Number of visible GPUs (0 when no GPU; never fails for lack of one). */
 int plk_device_count(int* out);
 int plk_ctx_create(int device, plk_ctx** out);

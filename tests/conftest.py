@@ -29,6 +29,8 @@ def plk():
     if not lib.exists():
         subprocess.run([sys.executable, str(ROOT / "dusk-plonk_amd" / "build_ext.py")], check=True)
     import dusk_plonk_amd
+    # the library must have been built from this tree's sources and flags (plk_build_info)
+    dusk_plonk_amd.check_build()
     return dusk_plonk_amd
 
 

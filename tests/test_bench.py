@@ -67,7 +67,7 @@ def test_kernel_mode_line_is_bit_exact(mode):
 @pytest.mark.gpu
 def test_prove_mode_line():
     d = run_bench("--log-n", "12", "--steps", "2", "--warmup", "1", "--lanes", "2",
-                  "--no-cpu-baseline")
+                  "--no-cpu-baseline", "--no-extras")
     check_contract(d, 2, 1)
     assert d["unit"] == "constraints/s" and d["scaling"] == "weak"
     # value counts every lane's proof: n * steps * lanes / time
@@ -116,7 +116,7 @@ def test_gpus_flag_must_match_launcher():
 @pytest.mark.gpu
 def test_prove_mode_line_has_solo_roofline():
     d = run_bench("--log-n", "12", "--steps", "2", "--warmup", "1", "--lanes", "2",
-                  "--no-cpu-baseline")
+                  "--no-cpu-baseline", "--no-extras")
     r = d["roofline"]
     assert r["kernel"] == "k_accumulate" and r["solo"]["launches"] == 4  # one proof
     assert r["avg_launch_ms"] == r["solo"]["avg_launch_ms"]
@@ -145,7 +145,7 @@ def test_gpus_2_shard_msm_launches_ranks_itself():
 def test_prove_mode_checks_its_proofs():
     """The prove line re-proves every lane's last timed proof alone and compares bytes."""
     d = run_bench("--log-n", "12", "--steps", "2", "--warmup", "1", "--lanes", "3",
-                  "--no-cpu-baseline")
+                  "--no-cpu-baseline", "--no-extras")
     assert d["proofs_checked"] == 3
     hc = d["host_cores"]
     assert hc["lanes_run"] == 3 and hc["needed_per_rank"] > 0 and hc["available_per_rank"] >= 1
@@ -221,7 +221,7 @@ def test_prove_line_world2_self_describing():
     """A multi-rank prove line (2 ranks sharing the card over gloo) carries every rank's
     roofline and the stored CPU baseline (bench.py stored_cpu_baseline), labelled as stored."""
     d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--log-n", "12", "--steps", "2",
-                  "--warmup", "1", "--lanes", "2", "--no-cpu-baseline", timeout=300)
+                  "--warmup", "1", "--lanes", "2", "--no-cpu-baseline", "--no-extras", timeout=300)
     check_contract(d, 2, 1, n_gpus=2)
     cb = d["cpu_baseline"]
     assert cb["source"].startswith("stored") and cb["value"] > 0 and cb["cores"] == 32
@@ -257,3 +257,104 @@ def test_msm_split_over_ranks_lines():
     assert d2["roofline"]["bucket_parts"]["parts"] == 2
     # one MSM per step whatever the world: value = n * steps / time
     assert d2["value"] == pytest.approx(65536 * 2 / (d2["ms_per_step"] * 2e-3), rel=1e-6)
+
+
+class _FakeSplitParams:
+    """CPU stand-in for the bench SRS in msm_shard_point: commit_batch_dev(part=, parts=)
+    returns the bucket-range share of the restated split (oracle/pyref.py msm_bucket_part,
+    c = 20), commit_dev the double-and-add MSM; scalars are read from the host pointer."""
+
+    def __init__(self, points):
+        self.points, self.n, self.parts_seen = points, len(points), []
+
+    @staticmethod
+    def _scalars(ptr, length):
+        import ctypes
+        import numpy as np
+        import pyref as P
+        a = np.ctypeslib.as_array((ctypes.c_uint64 * (4 * length)).from_address(ptr))
+        return P.fr_vec_from_np(a.reshape(length, 4).copy())
+
+    def commit_batch_dev(self, ptrs_lens, stream=0, raise_on_error=True, part=0, parts=1):
+        import pyref as P
+        import dusk_plonk_amd as plk
+        self.parts_seen.append((part, parts))
+        (ptr, length), = ptrs_lens
+        share = P.msm_bucket_part(self.points[:length], self._scalars(ptr, length), 20, part, parts)
+        return [plk.Commitment(P.g1_vec_to_np([share])[0])]
+
+    def commit_dev(self, ptr, length, stream=0):
+        import pyref as P
+        import dusk_plonk_amd as plk
+        return plk.Commitment(P.g1_vec_to_np([P.msm_naive(self.points[:length],
+                                                          self._scalars(ptr, length))])[0])
+
+
+def _msm_shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PLK_MSM_C="20")
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(ROOT / "oracle")]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import bench
+    import pyref as P
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = dict(np.load(ROOT / "tests" / "golden" / "msm_golden.npz", allow_pickle=False))
+        pp = _FakeSplitParams(P.g1_vec_from_np(g["srs"]))
+        r = bench.msm_shard_point(None, torch, dist, world, rank, "cpu", pp, 6, 2, 1, 1)
+        ok = r["parts"] == world and r["split"] == "bucket range" and r["bit_exact"] is True
+        ok &= len(r["per_rank_part_ms"]) == world and r["ms_per_msm"] > 0
+        ok &= r["points_per_s"] > 0 and set(pp.parts_seen) == {(rank, world)}
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_msm_shard_point_gloo_world2():
+    """The msm_shard field of the default multi-rank line (the north star's MSM curve): ONE
+    MSM per step split over 2 gloo ranks by bucket range, shares all-gathered and folded, the
+    fold checked against the unsplit commit on every rank (CPU: the split restated by pyref)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_msm_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    out = dict(q.get(timeout=5) for _ in range(2))
+    assert out == {0: True, 1: True}
+    for p in procs:
+        assert p.exitcode == 0
+
+
+@pytest.mark.gpu
+def test_prove_line_extras_world1():
+    """The default line's extras at world 1: msm_shard = the lone 2^k MSM (the curve's N = 1
+    point) checked against the oracle; n_2_16 = the metric's second size, proofs re-checked;
+    build_id = the library's source hash, equal to the tree's."""
+    d = run_bench("--log-n", "14", "--steps", "2", "--warmup", "1", "--lanes", "2",
+                  "--no-cpu-baseline", timeout=300)
+    m = d["msm_shard"]
+    assert m["parts"] == 1 and m["bit_exact"] is True and "oracle" in m["check"]
+    assert m["ms_per_msm"] > 0 and m["n"] == 1 << 14
+    s = d["n_2_16"]
+    assert s["log_n"] == 16 and s["value"] > 0 and s["proofs_checked"] == s["lanes"] == 14
+    assert d["build_id"]["src"] == d["build_id"]["tree_src"]
+
+
+@pytest.mark.gpu
+def test_prove_line_msm_curve_world2():
+    """At world 2 (two gloo ranks sharing the card) the line's msm_shard is ONE 2^16 MSM split
+    by bucket range over both ranks, folded and checked against the unsplit commit."""
+    d = run_bench("--gpus", "2", "--dist-backend", "gloo", "--log-n", "16", "--steps", "2",
+                  "--warmup", "1", "--lanes", "2", "--no-cpu-baseline", timeout=400)
+    m = d["msm_shard"]
+    assert m["parts"] == 2 and m["split"] == "bucket range" and m["bit_exact"] is True
+    assert len(m["per_rank_part_ms"]) == 2 and "n_2_16" not in d

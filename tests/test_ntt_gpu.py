@@ -46,6 +46,24 @@ def test_all_transforms_vs_oracle(plk, gpu_ctx, oracle, k):
     assert np.array_equal(f.coset_dft(plk.Coefficients(x[:m])).values, oracle.coset_dft(x[:m], k))
 
 
+@pytest.mark.parametrize("k", [12, 17, 20])
+def test_idft_multipass_identity_rows(plk, gpu_ctx, oracle, k):
+    """A multi-pass plain idft carries n^-1 on its last pass' inter-pass twiddles
+    (pass_tw_inv_last, round 5), so the j = 0 / k = 0 entries of that table are n^-1, not one
+    (ntt.hip: the multiply must stay unconditional). idft(all ones) = (1, 0, ..., 0) puts all
+    of the result on row 0; a skipped identity entry would leave n there."""
+    import pyref as P
+    n = 1 << k
+    f = plk.Fft(k, gpu_ctx)
+    delta = np.zeros((n, 4), dtype=np.uint64)
+    delta[0] = P.fr_vec_to_np([1])[0]
+    ones = oracle.dft(delta, k)
+    assert np.array_equal(ones, np.repeat(delta[:1], n, axis=0))
+    assert np.array_equal(f.idft(plk.PointsValue(ones)).values, delta)
+    x = random_fr(n, seed=7 + k)
+    assert np.array_equal(f.idft(plk.PointsValue(x)).values, oracle.idft(x, k))
+
+
 def test_empty_and_zero_inputs(plk, gpu_ctx):
     f = plk.Fft(6, gpu_ctx)
     z = np.zeros((0, 4), dtype=np.uint64)

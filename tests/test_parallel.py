@@ -670,3 +670,26 @@ def test_rccl_in_process_device_exchange(plk, gpu_ctx):
         assert svc.requests == 15
     finally:
         dist.destroy_process_group()
+
+
+def test_window_bits_mirror_choose_c(monkeypatch):
+    """parallel.window_bits / bucket_parts_ok follow srs.hip choose_c + msm_prepare_srs
+    (round-5 advisor: PLK_MSM_C = 18 runs as 17, 21 / 23 are refused, 2^14 / 2^13 points take
+    c = 13 / 12), checked against pyref.msm_effective_c."""
+    import pyref as P
+    from dusk_plonk_amd.parallel import bucket_parts_ok, window_bits
+
+    monkeypatch.delenv("PLK_MSM_C", raising=False)
+    for n, c in [((1 << 20) + 8, 20), ((1 << 16) + 8, 17), (1 << 15, 15), ((1 << 14) + 8, 13),
+                 (1 << 13, 12), (1 << 12, 10), (1 << 9, 8)]:
+        assert window_bits(n) == c
+    monkeypatch.setenv("PLK_MSM_C", "18")
+    assert window_bits(1 << 10) == 17 == P.msm_effective_c(18)
+    assert bucket_parts_ok(1 << 10, 4) and not bucket_parts_ok(1 << 10, 8)
+    for bad in ("21", "23", "7", "x"):
+        monkeypatch.setenv("PLK_MSM_C", bad)
+        assert window_bits(1 << 20) == 20 and window_bits(1 << 14) == 13
+    monkeypatch.setenv("PLK_MSM_C", "20")
+    assert bucket_parts_ok(1 << 10, 8) and not bucket_parts_ok(1 << 10, 64)
+    monkeypatch.delenv("PLK_MSM_C")
+    assert bucket_parts_ok(1 << 14, 1) and not bucket_parts_ok(1 << 14, 2)
