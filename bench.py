@@ -15,8 +15,9 @@ value = constraints/s = n * proofs / max-over-ranks time.
   * default: proof batches — every rank proves its own proofs (weak scaling, no
     data-path collective; torch.distributed only for the barrier and the max reduction);
   * --shard-msm (BASELINE configs[4]): every rank proves the SAME proofs and each commit is
-    split over the ranks by SRS slice (plk_prover_shard: one RCCL all-gather of partial
-    points per commit group, host fold) — strong scaling of proof latency.
+    split over the ranks by bucket range (plk_prover_shard_buckets, round 6) or, where the
+    SRS does not allow that split, by SRS slice (plk_prover_shard): one RCCL all-gather of
+    partial points per commit group, host fold — strong scaling of proof latency.
 `--gpus N` without a launcher starts N ranks itself (torch.distributed.run, 127.0.0.1).
 Other modes: hotpath (only the NTT/MSM calls of one proof), ntt / msm (BASELINE configs[1] /
 [2], checked bit-exact against the oracle after the timed loop).
@@ -123,9 +124,14 @@ def parse():
                          "gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--shard-msm", action="store_true",
                     help="BASELINE configs[4]: all ranks prove the same proofs, every commit "
-                         "split over the ranks by SRS slice (RCCL all-gather of partial points "
+                         "split over the ranks (--shard-split; RCCL all-gather of partial points "
                          "+ host fold); NTT / elementwise rounds replicated. With --mode msm: "
                          "ONE MSM per step split over the ranks (--msm-split)")
+    ap.add_argument("--shard-split", choices=["auto", "buckets", "slices"], default="auto",
+                    help="--shard-msm in prove mode: split every commit by bucket range "
+                         "(plk_prover_shard_buckets: every rank holds the whole SRS and reduces "
+                         "1/G of the buckets) or by SRS slice (plk_prover_shard); auto = buckets "
+                         "where the SRS allows G parts (c >= 17, >= 2^14 buckets per part)")
     ap.add_argument("--msm-split", choices=["buckets", "points"], default="buckets",
                     help="--mode msm --shard-msm: by bucket range (each rank sorts, accumulates "
                          "and reduces 1/G of the buckets; plk_commit_batch_dev_part) or by SRS "
@@ -842,17 +848,25 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
     lane_seed = (lambda l: 17 + 101 * l) if shard else (lambda l: 1000 * rank + 17 + 101 * l)
     lanes = [ProofLane(base, lane_seed(l)) for l in range(L)]
     exchange = None
+    split = None
     if shard:
-        from dusk_plonk_amd.parallel import ExchangeService, shard_prover_lane, srs_slice
+        from dusk_plonk_amd.parallel import (ExchangeService, bucket_parts_ok, shard_prover_lane,
+                                             srs_slice)
         comm_dev = device if dist.get_backend() == "nccl" else None
-        sl = srs_slice(base.tau, base.pp.n, world, rank, ctx)  # one slice per GPU, all lanes
+        # the split of every commit: by bucket range where the key's SRS allows it (round 6:
+        # each rank sorts, accumulates AND reduces 1/G of the buckets), else by SRS slice
+        split = args.shard_split
+        if split == "auto":
+            split = "buckets" if bucket_parts_ok(base.pp.n, world) else "slices"
+        sl = (srs_slice(base.tau, base.pp.n, world, rank, ctx)  # one slice per GPU, all lanes
+              if split == "slices" else None)
         # every lane's exchanges on ONE communicator, issued by ONE thread per rank in the
         # order rank 0 sequences (parallel.ExchangeService: no concurrent collectives on
         # different communicators, so no cross-rank ordering deadlock)
         exchange = ExchangeService(None, comm_dev)
         for l, ln in enumerate(lanes):
             shard_prover_lane(ln.lane, base.tau, base.pp.n, None, comm_dev, ctx, slice_=sl,
-                              exchange=exchange, lane_id=l)
+                              exchange=exchange, lane_id=l, mode=split)
     import concurrent.futures as cf
     drivers = cf.ThreadPoolExecutor(L)
 
@@ -932,12 +946,13 @@ def run_full(args, plk, torch, dist, world, rank, device, k, n, shard):
                         "the current GPU proof"
                         + (f"; {L} proofs in flight per GPU (plk_prover lanes sharing one key "
                            "and SRS)" if L > 1 else "")
-                        + (f"; every commit split over {world} GPU(s) by SRS slice "
-                           f"({transport(dist)} all-gather of partial points + host fold), NTT / elementwise "
-                           "rounds replicated on every GPU" if shard else ""),
+                        + (f"; every commit split over {world} GPU(s) by "
+                           + ("bucket range" if split == "buckets" else "SRS slice")
+                           + f" ({transport(dist)} all-gather of partial points + host fold), "
+                           "NTT / elementwise rounds replicated on every GPU" if shard else ""),
             "n": n, "log_n": k, "proofs_per_step": proofs,
-            "parallelism": (f"msm-shard x{world} x {L} lane(s), partials all-gathered over "
-                            f"{transport(dist)}" if shard else
+            "parallelism": (f"msm-shard x{world} ({split}) x {L} lane(s), partials all-gathered "
+                            f"over {transport(dist)}" if shard else
                             f"proof-batch x{world * L} ({L} concurrent prover lane(s) per GPU)")
                            + (f"; lanes lowered from {len(lanes_all)} to {L} (--fit-lanes: host "
                               "CPU share)" if L < len(lanes_all) else ""),

@@ -245,6 +245,10 @@ int msm_run(plk_srs* s, const Fr* d_scalars, size_t len, size_t check_len, plk_g
 int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const size_t* lens,
                   const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
                   hipStream_t stream, uint32_t part = 0, uint32_t parts = 1);
+// whether msm_run_batch accepts `parts` bucket ranges on this SRS (a power of two; for
+// parts > 1 a wide bucket set, 2^(c-1) above the LDS histogram's range, and >= 2^14 buckets
+// per part)
+bool msm_parts_ok(const plk_srs* s, uint32_t parts);
 MsmWorkspace* msm_workspace_new();
 void msm_workspace_delete(MsmWorkspace* w);
 const MsmStats& msm_workspace_stats(const MsmWorkspace& w);

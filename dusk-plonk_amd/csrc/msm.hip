@@ -1448,15 +1448,19 @@ static void bitsum_launch(bool wide, uint32_t G, uint32_t slots, uint32_t NR, ui
   }
 }
 
+bool msm_parts_ok(const plk_srs* s, uint32_t parts) {
+  if (parts == 0 || (parts & (parts - 1))) return false;
+  // a part's bucket range stays a wide set's (two-level sort, run sums): >= 2^14 buckets
+  return parts == 1 ||
+         ((1u << (s->c - 1)) > kLdsBuckets && ((1u << (s->c - 1)) / parts) >= (1u << 14));
+}
+
 int msm_run_batch(plk_srs* s, MsmWorkspace& w, const Fr* const* d_scalars, const size_t* lens,
                   const size_t* check_lens, size_t count, plk_g1* outs, int* statuses,
                   hipStream_t stream, uint32_t part, uint32_t parts) {
   if (count == 0) return PLK_OK;
   if (count > kMaxSlots) return PLK_E_ARG;
-  if (parts == 0 || (parts & (parts - 1)) || part >= parts) return PLK_E_ARG;
-  // a part's bucket range stays a wide set's (two-level sort, run sums): >= 2^14 buckets
-  if (parts > 1 && (((1u << (s->c - 1)) <= kLdsBuckets) || ((1u << (s->c - 1)) / parts) < (1u << 14)))
-    return PLK_E_ARG;
+  if (!msm_parts_ok(s, parts) || part >= parts) return PLK_E_ARG;
   size_t max_len = 0, max_tail = 0, total_entries = 0;
   MsmBatch batch{};
   for (size_t k = 0; k < count; ++k) {

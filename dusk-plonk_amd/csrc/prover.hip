@@ -328,13 +328,22 @@ int key_commit(plk_key* key, MsmWorkspace& ws, const std::vector<const Fr*>& ptr
 // tail starts relative to its slice (an SRS longer than the circuit's trimmed one puts the
 // last slice past it). Every rank takes part in the exchange even when its own MSMs failed,
 // so no rank waits forever on a collective the others left.
+// Bucket-range form (plk_prover_shard_buckets, round 6): every rank holds the key's whole SRS
+// and window table and runs each commit of the group over ALL of its points, keeping only the
+// digits of bucket range `rank` of `world` (msm_run_batch part / parts: its sort, accumulation
+// and run-sum / bit-sum reduction cover 1/world of the 2^(c-1) buckets); its outputs are that
+// range's shares, and the same exchange and fold give the commitments. Every part checks the
+// degree tail itself, so every rank sees the same status.
 int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
                  const std::vector<size_t>& lens, plk_g1* outs, int* statuses, size_t cap) {
   plk_key* key = P->key;
   const size_t cnt = ptrs.size();
   const size_t max_points = std::min<size_t>(std::min<size_t>(key->srs->n, key->n_trim), cap);
-  const uint64_t lo = P->shard_lo, hi = lo + P->shard->n;
-  const bool last = P->rank == P->world - 1;
+  const bool buckets = P->shard_buckets;
+  plk_srs* srs = buckets ? key->srs : P->shard;
+  const uint64_t lo = buckets ? 0 : P->shard_lo, hi = buckets ? key->srs->n : lo + P->shard->n;
+  const bool last = buckets || P->rank == P->world - 1;
+  const uint32_t part = buckets ? (uint32_t)P->rank : 0, parts = buckets ? (uint32_t)P->world : 1;
   std::vector<const Fr*> lp(cnt);
   std::vector<size_t> luse(cnt), lchk(cnt);
   int local = PLK_OK;
@@ -355,13 +364,13 @@ int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
       }
     }
   }
-  std::vector<plk_g1> part(cnt, plk_g1{});
+  std::vector<plk_g1> shares(cnt, plk_g1{});
   std::vector<int> pst(cnt, PLK_OK);
   for (size_t base = 0; local == PLK_OK && base < cnt; base += kMaxSlots) {
     const size_t m = std::min<size_t>(kMaxSlots, cnt - base);
-    const int r = msm_run_batch(P->shard, *P->ws, lp.data() + base, luse.data() + base,
-                                lchk.data() + base, m, part.data() + base, pst.data() + base,
-                                P->stream);
+    const int r = msm_run_batch(srs, *P->ws, lp.data() + base, luse.data() + base,
+                                lchk.data() + base, m, shares.data() + base, pst.data() + base,
+                                P->stream, part, parts);
     if (r != PLK_OK && r != PLK_E_DEGREE) local = r;
   }
   // payload per commit: x[6], y[6], infinity, status
@@ -369,7 +378,7 @@ int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
   std::vector<uint64_t> send(cnt * kWords), recv((size_t)P->world * cnt * kWords);
   for (size_t i = 0; i < cnt; ++i) {
     uint64_t* w = &send[i * kWords];
-    std::memcpy(w, &part[i], sizeof(plk_g1));
+    std::memcpy(w, &shares[i], sizeof(plk_g1));
     w[13] = (uint64_t)(local != PLK_OK ? local : pst[i]);
   }
   if (P->allgather(P->allgather_user, send.data(), send.size() * 8, recv.data()) != 0)
@@ -401,7 +410,7 @@ int shard_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
 int prover_commit(plk_prover* P, const std::vector<const Fr*>& ptrs,
                   const std::vector<size_t>& lens, plk_g1* outs, int* statuses,
                   size_t cap = SIZE_MAX) {
-  if (P->shard) return shard_commit(P, ptrs, lens, outs, statuses, cap);
+  if (P->shard || P->shard_buckets) return shard_commit(P, ptrs, lens, outs, statuses, cap);
   return key_commit(P->key, *P->ws, ptrs, lens, outs, statuses, P->stream, cap);
 }
 
@@ -974,9 +983,27 @@ int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int ra
     return PLK_E_ARG;
   p->shard = sharded ? slice : nullptr;
   p->shard_lo = sharded ? slice_start : 0;
+  p->shard_buckets = false;
   p->rank = rank;
   p->world = world;
   p->allgather = sharded ? allgather : nullptr;
+  p->allgather_user = user;
+  return PLK_OK;
+}
+
+int plk_prover_shard_buckets(plk_prover* p, int rank, int world, plk_allgather_fn allgather,
+                             void* user) {
+  if (!p || !allgather || world < 1 || rank < 0 || rank >= world) return PLK_E_ARG;
+  // msm_run_batch's part conditions (a power of two; a wide bucket set, c >= 17, with >= 2^14
+  // buckets per part); otherwise the caller keeps SRS slices (parallel.shard_prover_lane
+  // mode "auto")
+  if (!msm_parts_ok(p->key->srs, (uint32_t)world)) return PLK_E_ARG;
+  p->shard = nullptr;
+  p->shard_lo = 0;
+  p->shard_buckets = true;
+  p->rank = rank;
+  p->world = world;
+  p->allgather = allgather;
   p->allgather_user = user;
   return PLK_OK;
 }

@@ -266,6 +266,9 @@ struct plk_prover {
   // sharded commits (plk_prover_shard): this rank's SRS slice and the all-gather
   plk_srs* shard = nullptr;
   uint64_t shard_lo = 0;
+  // plk_prover_shard_buckets (round 6): every commit on the key's own (whole) SRS, this rank
+  // keeping bucket range `rank` of `world` (msm_run_batch part / parts) instead of a slice
+  bool shard_buckets = false;
   int rank = 0, world = 1;
   plk_allgather_fn allgather = nullptr;
   void* allgather_user = nullptr;

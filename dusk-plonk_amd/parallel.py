@@ -293,19 +293,35 @@ def srs_slice(tau, n_points: int, world: int, rank: int, ctx=None):
 
 
 def shard_prover_lane(lane, tau, n_points: int, group=None, device=None, ctx=None,
-                      slice_=None, exchange: ExchangeService | None = None, lane_id: int = 0):
-    """Split every commit of `lane` (a prover.ProverLane) over the ranks of `group`: this
-    rank's slice of the first `n_points` SRS powers of `tau` and an all-gather.
-    `slice_` = (start, PlonkParams) from srs_slice lets several lanes share one slice (the
-    SRS is read-only; each lane brings its own MSM workspace). With several lanes per rank
-    pass `exchange` (one ExchangeService per rank) and a `lane_id` that names the same lane
-    on every rank: all lanes' exchanges then share one communicator and one issuing thread.
-    A lone lane may use the group's all-gather directly. Returns the slice."""
+                      slice_=None, exchange: ExchangeService | None = None, lane_id: int = 0,
+                      mode: str = "slices"):
+    """Split every commit of `lane` (a prover.ProverLane) over the ranks of `group`, one
+    all-gather per commit group, two ways:
+
+    * mode "slices" (rounds 2-5, plk_prover_shard): this rank's slice of the first `n_points`
+      SRS powers of `tau`; `slice_` = (start, PlonkParams) from srs_slice lets several lanes
+      share one slice (the SRS is read-only; each lane brings its own MSM workspace);
+    * mode "buckets" (round 6, plk_prover_shard_buckets): the key's own whole SRS, this rank
+      keeping bucket range `rank` of `world` of every commit (its sort, accumulation and
+      bucket reduction cover 1/world of the buckets; no slice is built). Needs a power-of-two
+      world and a wide bucket set with >= 2^14 buckets per part (bucket_parts_ok);
+    * mode "auto": buckets where the key's SRS allows the split, slices otherwise (the same
+      decision on every rank: it depends only on the SRS size and the world).
+
+    With several lanes per rank pass `exchange` (one ExchangeService per rank) and a `lane_id`
+    that names the same lane on every rank: all lanes' exchanges then share one communicator
+    and one issuing thread. A lone lane may use the group's all-gather directly. Returns the
+    slice (start, PlonkParams), or None in bucket mode."""
     import torch.distributed as dist
 
+    if mode not in ("slices", "buckets", "auto"):
+        raise ValueError(f"shard_prover_lane: mode {mode!r}")
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    lo, sl = slice_ if slice_ is not None else srs_slice(tau, n_points, world, rank, ctx)
     ag = exchange.allgather_for(lane_id) if exchange is not None else torch_allgather(group, device)
+    if mode == "buckets" or (mode == "auto" and bucket_parts_ok(lane.prover.pp.n, world)):
+        lane.shard(None, 0, rank, world, ag, buckets=True)
+        return None
+    lo, sl = slice_ if slice_ is not None else srs_slice(tau, n_points, world, rank, ctx)
     lane.shard(sl, lo, rank, world, ag)
     return lo, sl
 

@@ -54,7 +54,7 @@ ABI_SYMBOLS = (
     "plk_composer_public_inputs", "plk_composer_export", "plk_key_compile", "plk_key_destroy",
     "plk_key_info",
     "plk_prove", "plk_prover_create", "plk_prover_destroy", "plk_prover_stream",
-    "plk_prover_prove", "plk_prover_msm_stats", "plk_prover_shard",
+    "plk_prover_prove", "plk_prover_msm_stats", "plk_prover_shard", "plk_prover_shard_buckets",
     "plk_proof_encode", "plk_proof_decode",
 )
 

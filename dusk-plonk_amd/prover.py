@@ -87,6 +87,7 @@ def _bind():
         "plk_prover_msm_stats": [vp, i32, C.POINTER(C.c_double), C.POINTER(u64),
                                  C.POINTER(u64), C.POINTER(u64)],
         "plk_prover_shard": [vp, vp, u64, i32, i32, vp, vp],  # fn: ALLGATHER_FN cast
+        "plk_prover_shard_buckets": [vp, i32, i32, vp, vp],
         "plk_proof_encode": [vp, vp, sz, C.POINTER(sz)],
         "plk_proof_decode": [vp, sz, vp],
     }
@@ -613,11 +614,14 @@ class ProverLane:
         _check(_bind().plk_prover_stream(self._h, C.byref(s)), "plk_prover_stream")
         return s.value or 0
 
-    def shard(self, slice_params, slice_start: int, rank: int, world: int, allgather):
-        """Split every commit of this lane's proofs over `world` ranks (plk_prover_shard):
-        `slice_params` is this rank's PlonkParams slice (PlonkParams.setup_range) starting
-        at SRS index `slice_start`; `allgather(send: bytes) -> bytes` returns the
-        concatenation of every rank's `send` in rank order."""
+    def shard(self, slice_params, slice_start: int, rank: int, world: int, allgather,
+              buckets: bool = False):
+        """Split every commit of this lane's proofs over `world` ranks: by SRS slice
+        (plk_prover_shard: `slice_params` is this rank's PlonkParams slice, PlonkParams.setup_range,
+        starting at SRS index `slice_start`) or, with buckets=True, by bucket range on the key's
+        own SRS (plk_prover_shard_buckets; slice_params / slice_start unused; PlonkError
+        PLK_E_ARG where the key's SRS cannot be split `world` ways). `allgather(send: bytes) ->
+        bytes` returns the concatenation of every rank's `send` in rank order."""
         def cb(_user, send, nbytes, recv):
             try:
                 data = allgather(C.string_at(send, nbytes))
@@ -630,6 +634,11 @@ class ProverLane:
                 traceback.print_exc()
                 return 1
         fn = ALLGATHER_FN(cb)
+        if buckets:
+            _check(_bind().plk_prover_shard_buckets(self._h, rank, world, C.cast(fn, C.c_void_p),
+                                                    None), "plk_prover_shard_buckets")
+            self._shard_keep = (fn, None)  # keep the callback alive
+            return
         self._shard_keep = (fn, slice_params)  # keep the callback and the slice alive
         _check(_bind().plk_prover_shard(self._h, slice_params._h if slice_params else None,
                                         slice_start, rank, world, C.cast(fn, C.c_void_p), None),

@@ -318,6 +318,17 @@ int plk_prover_msm_stats(plk_prover* p, int reset, double* accumulate_ms, uint64
 typedef int (*plk_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
 int plk_prover_shard(plk_prover* p, plk_srs* slice, uint64_t slice_start, int rank, int world,
                      plk_allgather_fn allgather, void* user);
+/* The same sharded proof with each commit split by BUCKET RANGE instead of SRS slice (round 6;
+ * the north star's "partial bucket sums"): every rank keeps the key's whole SRS and window
+ * table and runs every commit of the group over all of its points, sorting, accumulating and
+ * reducing only bucket range `rank` of `world` (plk_commit_batch_dev_part's split, so each rank
+ * also does 1/world of the bucket reduction, which the slice split repeats on every rank); the
+ * shares go through the same all-gather and fold, so proofs are byte-identical. PLK_E_ARG
+ * unless `world` is a power of two and the key's SRS has a wide bucket set with >= 2^14
+ * buckets per part (c >= 17: SRS >= 2^16 points; c = 20 from 2^20 points: world <= 32) — the
+ * caller then keeps plk_prover_shard's slices. Undone by plk_prover_shard. */
+int plk_prover_shard_buckets(plk_prover* p, int rank, int world, plk_allgather_fn allgather,
+                             void* user);
 
 /* ---- Proof wire format (SCALE, src/prover/proof.rs:11,36) ---------------------------------
  * The reference derives parity-scale-codec Encode/Decode for Proof: fields in declaration

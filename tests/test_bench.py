@@ -136,7 +136,7 @@ def test_gpus_2_shard_msm_launches_ranks_itself():
                   timeout=300)
     check_contract(d, 2, 1, n_gpus=2)
     assert d["scaling"] == "strong" and d["config"]["proofs_per_step"] == 2
-    assert d["config"]["parallelism"].startswith("msm-shard x2")
+    assert d["config"]["parallelism"].startswith("msm-shard x2 (slices)")  # c = 10: no bucket split
     # all ranks prove the same proofs: value counts each once
     assert d["value"] == pytest.approx(4096 * 2 * 2 / (d["ms_per_step"] * 2e-3), rel=1e-6)
 
@@ -358,3 +358,15 @@ def test_prove_line_msm_curve_world2():
     m = d["msm_shard"]
     assert m["parts"] == 2 and m["split"] == "bucket range" and m["bit_exact"] is True
     assert len(m["per_rank_part_ms"]) == 2 and "n_2_16" not in d
+
+
+@pytest.mark.gpu
+def test_gpus_2_shard_msm_bucket_split():
+    """configs[4] with the bucket-range split (plk_prover_shard_buckets): 2^16 (c = 17, 2 parts
+    of 2^15 buckets), two gloo ranks sharing the card, every lane's proof re-checked alone."""
+    d = run_bench("--gpus", "2", "--shard-msm", "--dist-backend", "gloo", "--log-n", "16",
+                  "--steps", "2", "--warmup", "1", "--lanes", "2", "--no-cpu-baseline",
+                  timeout=400)
+    check_contract(d, 2, 1, n_gpus=2)
+    assert d["config"]["parallelism"].startswith("msm-shard x2 (buckets)")
+    assert "bucket range" in d["config"]["workload"] and d["proofs_checked"] == 2

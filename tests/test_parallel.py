@@ -217,7 +217,7 @@ def test_msm_sharded_single_process(plk, gpu_ctx):
             assert np.array_equal(msm_sharded(shards, sc[:m]).words, full.msm(sc[:m]).words), (cuts, m)
 
 
-def _sharded_prover_worker(rank, world, port, q, logn):
+def _sharded_prover_worker(rank, world, port, q, logn, mode="slices"):
     """BASELINE configs[4] at a test size: every rank proves the same circuit with its
     commits split by SRS slice (plk_prover_shard) and exchanges partials over gloo; the
     proof must equal the unsharded plk_prove's byte for byte on every rank."""
@@ -243,7 +243,7 @@ def _sharded_prover_worker(rank, world, port, q, logn):
             return cs
         prover, _ = PlonkKey.compile_composer(pp, b"shard", circ(1))
         lane = prover.lane()
-        shard_prover_lane(lane, tau, pp.n, None, None, ctx)
+        shard_prover_lane(lane, tau, pp.n, None, None, ctx, mode=mode)
         ok = True
         for seed in (3, 4):
             want = prover.prove_composer(circ(seed + 10), seed)[0].raw_bytes()
@@ -274,6 +274,55 @@ def test_sharded_prover_two_ranks_wide_slices(plk, gpu_ctx):
     """2^17: each rank's SRS slice holds over 2^16 points, so the sharded commits run the
     MSM's wide-bucket path (c = 17: two-level sort, run-sum reduction) on every rank."""
     out = _spawn(_sharded_prover_worker, 2, 17)
+    assert out == {0: True, 1: True}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_prover_bucket_split(plk, gpu_ctx, world):
+    """plk_prover_shard_buckets (round 6): every commit of a 2^17 proof split by bucket range
+    (c = 17: 2 or 4 parts of 2^15 / 2^14 buckets) over gloo ranks sharing the card; proofs equal
+    plk_prove's bytes and an unsatisfied circuit fails with the degree error on every rank."""
+    out = _spawn(_sharded_prover_worker, world, 17, "buckets")
+    assert out == {r: True for r in range(world)}
+
+
+def _bucket_refusal_worker(rank, world, port, q):
+    """mode "buckets" is refused (PLK_E_ARG) where the key's SRS has no wide bucket set
+    (2^12: c = 10); mode "auto" then shards by slice and proves the same bytes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests")]
+    import torch.distributed as dist
+    from oracle_lib import random_fr
+    import dusk_plonk_amd as plk
+    from dusk_plonk_amd.parallel import shard_prover_lane
+    from dusk_plonk_amd.prover import Plonk, PlonkKey
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tau = random_fr(1, seed=95)[0]
+        ctx = plk.Context.default(0)
+        pp = plk.PlonkParams.setup(12, tau, ctx)
+        cs = Plonk()
+        cs.synthetic_chain((1 << 12) - 15, 3)
+        prover, _ = PlonkKey.compile_composer(pp, b"refuse", cs)
+        lane = prover.lane()
+        ok = False
+        try:
+            shard_prover_lane(lane, tau, pp.n, mode="buckets")
+        except plk.PlonkError as e:
+            ok = e.status == plk.PLK_E_ARG
+        ok &= shard_prover_lane(lane, tau, pp.n, ctx=ctx, mode="auto") is not None  # a slice
+        ok &= lane.prove_composer(cs, 9)[0].raw_bytes() == prover.prove_composer(cs, 9)[0].raw_bytes()
+        lane.close()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_prover_bucket_split_refused_small_srs(plk, gpu_ctx):
+    out = _spawn(_bucket_refusal_worker, 2)
     assert out == {0: True, 1: True}
 
 
@@ -329,6 +378,54 @@ def _allgather_cb_worker(rank, world, port, q):
 
 def test_sharded_prover_exchange_gloo_world2():
     out = _spawn(_allgather_cb_worker, 2)
+    assert out == {0: True, 1: True}
+
+
+def _bucket_exchange_worker(rank, world, port, q):
+    """The bucket-split prover's exchange (plk_prover_shard_buckets) without a GPU: each
+    rank's payload is its bucket-range shares of several commits (restated split,
+    oracle/pyref.py msm_bucket_part at c = 20), 13 point words + a status word each, sent
+    through the same ctypes all-gather callback the C++ prover calls and folded with
+    plk_g1_sum; a degree status on one rank must reach every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(ROOT / "oracle")]
+    import ctypes as C
+    import torch.distributed as dist
+    import pyref as P
+    import dusk_plonk_amd as plk
+    from dusk_plonk_amd.parallel import torch_allgather
+    from dusk_plonk_amd.prover import ALLGATHER_FN
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = dict(np.load(ROOT / "tests" / "golden" / "msm_golden.npz", allow_pickle=False))
+        pts = P.g1_vec_from_np(g["srs"])
+        ag = torch_allgather()
+
+        def cb(_u, send, nbytes, recv):
+            data = ag(C.string_at(send, nbytes))
+            C.memmove(recv, data, len(data))
+            return 0
+        fn = ALLGATHER_FN(cb)
+        slots = ["random", "sparse", "high_bits"]
+        send = np.zeros((len(slots) + 1, 14), dtype=np.uint64)
+        for i, sname in enumerate(slots):
+            sc = P.fr_vec_from_np(g[f"{sname}_scalars"])
+            send[i, :13] = P.g1_vec_to_np([P.msm_bucket_part(pts, sc, 20, rank, world)])[0]
+        send[-1, 12] = 1
+        send[-1, 13] = plk.PLK_E_DEGREE if rank == world - 1 else plk.PLK_OK
+        recv = np.zeros((world, len(slots) + 1, 14), dtype=np.uint64)
+        ok = fn(None, send.ctypes.data, send.nbytes, recv.ctypes.data) == 0
+        for i, sname in enumerate(slots):
+            ok &= np.array_equal(plk.plonk.g1_sum(recv[:, i, :13]).words, g[f"{sname}_result"])
+        ok &= int(recv[:, -1, 13].max()) == plk.PLK_E_DEGREE
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_split_prover_exchange_gloo_world2():
+    out = _spawn(_bucket_exchange_worker, 2)
     assert out == {0: True, 1: True}
 
 
@@ -501,7 +598,7 @@ def test_sharded_prover_three_ranks_large_srs(plk, gpu_ctx):
     assert out == {0: True, 1: True, 2: True}
 
 
-def _sharded_2_20_worker(rank, world, port, q):
+def _sharded_2_20_worker(rank, world, port, q, mode="slices"):
     """BASELINE configs[4] at its own size: the headline 2^20 bench circuit proved with every
     commit split over the ranks (plk_prover_shard, gloo on one card here; RCCL over xGMI on a
     node), byte for byte against the committed oracle fixture tests/golden/proof_2_20.npz."""
@@ -525,7 +622,7 @@ def _sharded_2_20_worker(rank, world, port, q):
         ok = np.array_equal(vd.comms, g["vk"])
         lane = prover.lane()
         svc = ExchangeService()
-        shard_prover_lane(lane, tau, pp.n, ctx=ctx, exchange=svc, lane_id=0)
+        shard_prover_lane(lane, tau, pp.n, ctx=ctx, exchange=svc, lane_id=0, mode=mode)
         proof, _ = lane.prove_composer(cs, BLIND_SEED)
         svc.close()
         ok &= proof.to_bytes() == g["scale"].tobytes()
@@ -538,6 +635,14 @@ def _sharded_2_20_worker(rank, world, port, q):
 @pytest.mark.gpu
 def test_sharded_prover_2_20_equals_fixture(plk, gpu_ctx):
     out = _spawn(_sharded_2_20_worker, 2)
+    assert out == {0: True, 1: True}
+
+
+@pytest.mark.gpu
+def test_sharded_prover_2_20_bucket_split_equals_fixture(plk, gpu_ctx):
+    """configs[4] with every commit split by bucket range (plk_prover_shard_buckets: c = 20,
+    2 parts of 2^18 buckets), byte for byte against the committed 2^20 oracle proof."""
+    out = _spawn(_sharded_2_20_worker, 2, "buckets")
     assert out == {0: True, 1: True}
 
 
