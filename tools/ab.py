@@ -72,7 +72,7 @@ def main() -> int:
         for args in a.args:
             for tag, ve in variants:
                 cmd = [sys.executable, "bench.py", *args.split(), "--warmup", str(a.warmup),
-                       "--no-cpu-baseline"]
+                       "--no-cpu-baseline", "--no-extras"]
                 r = subprocess.run(["timeout", "-k", "10", str(a.timeout), *cmd], cwd=ROOT,
                                    env={**base_env, **ve}, capture_output=True, text=True)
                 if r.returncode != 0:
