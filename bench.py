@@ -727,7 +727,7 @@ def msm_shard_point(plk, torch, dist, world, rank, device, pp, k, steps, warmup,
     sync = torch.cuda.synchronize if gpu else (lambda: None)
     x = rand_fr_dev(torch, n, 4343, device)
     split = world > 1 and bucket_parts_ok(pp.n, world)
-    comm_dev = device if dist.get_backend() == "nccl" else None
+    comm_dev = device if split and dist.get_backend() == "nccl" else None
     coms, part_s = [], []
 
     def one(timed):
