@@ -156,7 +156,8 @@ def r_ab(o, a):
     tools/ab.py. Every round-5 gpu_r05_<x>.sh A/B was one or two of these (tools/README.md maps
     them)."""
     cmd = [PY, "-u", "tools/ab.py", "--out", str(o / "ab.jsonl"), "--reps", str(a.reps)]
-    for flag, vals in (("--lib", a.lib), ("--venv", a.venv), ("--args", a.args), ("--tests", a.tests)):
+    for flag, vals in (("--lib", a.lib), ("--venv", a.venv), ("--args", a.args), ("--tests", a.tests),
+                       ("--env", a.env)):
         for v in vals:
             cmd += [flag, v]
     run(cmd, a.limit)
@@ -185,6 +186,9 @@ def main() -> int:
     ap.add_argument("--venv", action="append", default=[])
     ap.add_argument("--args", action="append", default=[])
     ap.add_argument("--tests", action="append", default=[])
+    ap.add_argument("--env", action="append", default=[],
+                    help="KEY=VALUE for every run of recipe ab (e.g. PLK_LIB_ANY_SRC=1 for a library "
+                         "built from another tree)")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--limit", type=int, default=1100)
     ap.add_argument("--sizes", default="12 14 16 18 20")
