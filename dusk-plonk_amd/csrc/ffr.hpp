@@ -407,30 +407,13 @@ enum : int { kRxMul = 0, kRxSqr = 1, kRxMulAdd = 2 };
 // from the asm (two-product groups): one wait cycle, against the 64-bit merge add per column
 // it replaces. A use-only pin ("v" input) leaves the order to the scheduler, which
 // regroups the chains: measured no faster than the plain code (profiles/r04_ubench_acc_pins.txt).
+// Round 6 measured what that padding costs (profiles/r06_nop_cost_ab.jsonl, 2^20 proofs, two
+// interleaved runs): one more s_nop 0 per step (+3 040 per mixed addition) took the lane form
+// of k_accumulate from 6.76 to 6.24e9 additions/s, i.e. ~0.5 issue cycle per s_nop, so the ~440
+// it pays are ~1 % of the kernel. Each step written as an inline-asm v_mad_u64_u32 instead (no
+// pins; every asm also defines vcc, which the hazard recognizer pads after) drew 2 297 s_nop and
+// ran 6.64e9: not kept (commit 3100a20 has both probes).
 PLK_RX void rx_pin(uint64_t& v) { __asm__ volatile("" : "+v"(v)); }
-
-#ifndef PLK_RX_ASM_MAD
-#define PLK_RX_ASM_MAD 0
-#endif
-// PLK_RX_ASM_MAD (round 6): each step of a product group is ONE v_mad_u64_u32 written as
-// inline asm (the accumulator tied in and out, the carry-out to vcc) instead of a plain
-// multiply-add followed by an empty pin: the asm itself keeps LLVM from reassociating the
-// chain, and the interleaved chains put an independent instruction between a chain's asm and
-// its next read (the one wait state the hazard recognizer assumes after any inline asm).
-// `first`: the accumulator starts here (s2 / s3, or the first column's product), no addend.
-PLK_RX void rx_madd_asm(uint64_t& acc, uint32_t x, uint32_t y, bool first) {
-  if (first)
-    __asm__("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=&v"(acc) : "v"(x), "v"(y) : "vcc");
-  else
-    __asm__("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y) : "vcc");
-}
-// the same with a constant second factor (a limb of p) in an SGPR (one SGPR per VOP3)
-PLK_RX void rx_madd_asm_s(uint64_t& acc, uint32_t x, uint32_t y, bool first) {
-  if (first)
-    __asm__("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=&v"(acc) : "v"(x), "s"(y) : "vcc");
-  else
-    __asm__("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "s"(y) : "vcc");
-}
 
 template <class C, int NP>
 struct RxGroupState {
@@ -525,29 +508,6 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
     const bool split = SPLIT_ON && (kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K]);
     const int t = pos[q]++;
     uint64_t& dst = which == 0 ? g.acc[p] : which == 1 ? s2[p] : s3[p];
-#if PLK_RX_ASM_MAD
-    // the accumulator's t-th term as (x, y), then one asm mad
-    uint32_t mx, my;
-    const int nprod_ = which != 0 ? 0 : kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? nsq
-                                      : (split ? n1 : 2 * n1);
-    const bool first = t == 0 && (which != 0 || K == 0);
-    if (which == 2) {
-      mx = c[p]->v[i0 + t]; my = d[p]->v[K - i0 - t];
-    } else if (which == 1 || t >= nprod_) {
-      const int i = rfirst + (which == 1 ? t : t - nprod_);
-      rx_madd_asm_s(dst, g.m[p][i], KC.p[K - i], first);
-      continue;
-    } else if (kind[p] == kRxSqr) {
-      if (t < ncross) { mx = a[p]->v[i0 + t]; my = g.a2[p][K - i0 - t]; }
-      else { mx = a[p]->v[K / 2]; my = a[p]->v[K / 2]; }
-    } else if (t < n1) {
-      mx = a[p]->v[i0 + t]; my = b[p]->v[K - i0 - t];
-    } else {
-      mx = c[p]->v[i0 + t - n1]; my = d[p]->v[K - i0 - t + n1];
-    }
-    rx_madd_asm(dst, mx, my, first);
-    continue;
-#endif
     // the accumulator's t-th term
     const int nprod = which != 0 ? 0 : kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? nsq
                                      : (split ? n1 : 2 * n1);
@@ -565,9 +525,6 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
       rx_madd(dst, c[p]->v[i0 + t - n1], d[p]->v[K - i0 - t + n1]);
     }
     rx_pin(dst);
-#ifdef PLK_EXTRA_NOPS  // cost probe (round 6): one more s_nop 0 per product-group step
-    __asm__ volatile("s_nop 0");
-#endif
   }
   (void)rlast;
 #pragma unroll

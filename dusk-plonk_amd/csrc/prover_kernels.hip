@@ -537,42 +537,46 @@ __global__ void __launch_bounds__(kEvalThreads) k_eval_final(const Fr* __restric
 // suffix scan of the sums over the threads (LDS) gives each thread the sum of y above its
 // range; pass 2 walks its range downward with that running sum (2 products per element there
 // instead of 4: y_j is read back, not recomputed; 2^12 proofs within noise of the round-3 form,
-// profiles/r04_ruffini_park_ab.jsonl). Start powers z^(tE) and z^-(tE+1) come from
-// product scans of z^E / z^-E in LDS. All powers R'-domain (the host converts), products in
-// the R domain, outputs canonical: the same field values as the five-dispatch form.
+// profiles/r04_ruffini_park_ab.jsonl). Start powers z^(tE) and z^-(tE+1) (round 6): t = 32 hi +
+// lo, so z^(tE) = z^(E lo) z^(32E hi); two waves first build the four 32-entry tables
+// z^(E i), z^(32E i), z^-(E i), z^-(32E i) from the host's binary powers (5 products each, in
+// parallel), then every thread takes 2 (3) products — 6 dependent products and one barrier
+// where the product scans of z^E / z^-E in LDS took 10 levels and 20 barriers. All powers
+// R'-domain (the host converts), products in the R domain, outputs canonical: the same field
+// values as the five-dispatch form.
 constexpr uint32_t kRuffiniThreads = 1024, kRuffiniSingleMax = 16 * kRuffiniThreads;
+static_assert(kRuffiniThreads == 32 * 32, "start powers: t = 32 hi + lo");
+struct RuffiniPow {
+  Fr up[10];  // z^(E 2^b), R'-domain
+  Fr dn[10];  // z^-(E 2^b), R'-domain
+};
 __global__ void __launch_bounds__(kRuffiniThreads) k_ruffini_single(const Fr* __restrict__ c, uint64_t len,
-                                                                    uint32_t E, Fr z, Fr zE, Fr zi,
-                                                                    Fr ziE, Fr* __restrict__ q) {
-  __shared__ Fr T[kRuffiniThreads], U[kRuffiniThreads];
+                                                                    uint32_t E, Fr z, Fr zi,
+                                                                    RuffiniPow pw2, Fr* __restrict__ q) {
+  __shared__ Fr P[4][32];
+  __shared__ Fr W[kRuffiniThreads / 64];
   const uint32_t tid = threadIdx.x;
-  // word by word: a select between two by-value argument structs took their addresses and
-  // staged both in scratch memory (80 B per lane)
-  const Fr one = rx_pack(rx_one<FrCfg>());
-  Fr t0, u0;
+  if (tid < 128) {  // table tb (0: z^(E i), 1: z^(32E i), 2 / 3: the inverses), entry i
+    const uint32_t tb = tid >> 5, i = tid & 31;
+    RFr v = rx_one<FrCfg>();
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    t0.v[i] = tid ? zE.v[i] : one.v[i];
-    u0.v[i] = tid ? ziE.v[i] : zi.v[i];
-  }
-  T[tid] = t0;
-  U[tid] = u0;
-  __syncthreads();
-  for (uint32_t h = 1; h < kRuffiniThreads; h <<= 1) {  // inclusive product scans
-    const RFr a = tid >= h ? rx_unpack(T[tid - h]) : rx_one<FrCfg>();
-    const RFr b = tid >= h ? rx_unpack(U[tid - h]) : rx_one<FrCfg>();
-    __syncthreads();
-    if (tid >= h) {
-      T[tid] = rx_pack(rx_mul(rx_unpack(T[tid]), a));
-      U[tid] = rx_pack(rx_mul(rx_unpack(U[tid]), b));
+    for (int b = 0; b < 5; ++b) {
+      Fr f;  // word by word (a lane-dependent pick of a by-value argument goes through scratch)
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        f.v[k] = tb < 2 ? (tb == 0 ? pw2.up[b].v[k] : pw2.up[b + 5].v[k])
+                        : (tb == 2 ? pw2.dn[b].v[k] : pw2.dn[b + 5].v[k]);
+      const RFr m = rx_mul(v, rx_unpack(f));
+      if ((i >> b) & 1) v = m;
     }
-    __syncthreads();
+    P[tb][i] = rx_pack(v);
   }
+  __syncthreads();
   const uint64_t j0 = (uint64_t)tid * E;
   const uint64_t j1 = j0 + E < len ? j0 + E : (j0 < len ? len : j0);
   const RFr zr = rx_unpack(z), zir = rx_unpack(zi);
-  RFr pw = rx_unpack(T[tid]);   // z^j0
-  RFr pwi = rx_unpack(U[tid]);  // z^-(j0 + 1)
+  RFr pw = rx_mul(rx_unpack(P[0][tid & 31]), rx_unpack(P[1][tid >> 5]));  // z^j0
+  RFr pwi = rx_mul(rx_mul(zir, rx_unpack(P[2][tid & 31])), rx_unpack(P[3][tid >> 5]));  // z^-(j0 + 1)
   Fr loc = fe_zero<FrCfg>(), ylast = fe_zero<FrCfg>();
   for (uint64_t j = j0; j < j1; ++j) {  // pass 1: this thread's sum of y_j
     const Fr y = rx_pack_canonical(rx_mul(ldr(&c[j]), pw));
@@ -584,16 +588,21 @@ __global__ void __launch_bounds__(kRuffiniThreads) k_ruffini_single(const Fr* __
     pw = rx_mul(pw, zr);
     pwi = rx_mul(pwi, zir);
   }
-  __syncthreads();  // T free again
-  T[tid] = loc;
-  __syncthreads();
-  for (uint32_t h = 1; h < kRuffiniThreads; h <<= 1) {  // inclusive suffix sums over threads
-    const Fr o = tid + h < kRuffiniThreads ? T[tid + h] : fe_zero<FrCfg>();
-    __syncthreads();
-    T[tid] = fe_add(T[tid], o);
-    __syncthreads();
+  // inclusive suffix sums of the threads' sums: inside each wave by cross-lane shuffles, then
+  // the totals of the waves above from LDS (one barrier instead of a 10-level LDS scan's 20)
+  Fr v = loc;
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (uint32_t h = 1; h < 64; h <<= 1) {
+    Fr o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o.v[k] = (uint32_t)__shfl_down((int)v.v[k], h, 64);
+    if (lane + h < 64) v = fe_add(v, o);
   }
-  Fr run = fe_sub(T[tid], loc);  // sum of y_i over i >= j1
+  if (lane == 0) W[wave] = v;
+  __syncthreads();
+  Fr run = fe_sub(v, loc);  // sum of y_i over i >= j1: this wave's part ...
+  for (uint32_t w = wave + 1; w < kRuffiniThreads / 64; ++w) run = fe_add(run, W[w]);  // ... the rest
   // pass 2, downward from j1 - 1: pwi = z^-(j1 + 1) -> z^-(k + 1); y_k back from q[k]
   for (uint64_t k = j1; k-- > j0;) {
     pwi = rx_mul(pwi, zr);
@@ -814,9 +823,16 @@ int pk_ruffini(const Fr* c, uint64_t len, const Fr& z, Fr* q, Fr* tmp, Fr* scan_
   if (len <= kRuffiniSingleMax) {  // one dispatch (k_ruffini_single)
     const uint32_t E = (uint32_t)((len + kRuffiniThreads - 1) / kRuffiniThreads);
     const Fr zinv = fe_inv(z);
+    RuffiniPow pw2;
+    Fr up = fe_pow_u64(z, E), dn = fe_pow_u64(zinv, E);
+    for (int b = 0; b < 10; ++b) {
+      pw2.up[b] = fe_to_rx_domain(up);
+      pw2.dn[b] = fe_to_rx_domain(dn);
+      up = fe_sqr(up);
+      dn = fe_sqr(dn);
+    }
     hipLaunchKernelGGL(k_ruffini_single, dim3(1), dim3(kRuffiniThreads), 0, s, c, len, E,
-                       fe_to_rx_domain(z), fe_to_rx_domain(fe_pow_u64(z, E)), fe_to_rx_domain(zinv),
-                       fe_to_rx_domain(fe_pow_u64(zinv, E)), q);
+                       fe_to_rx_domain(z), fe_to_rx_domain(zinv), pw2, q);
     PLK_HIP_TRY(hipGetLastError());
     return PLK_OK;
   }

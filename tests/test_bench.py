@@ -257,6 +257,18 @@ def test_msm_split_over_ranks_lines():
     assert d2["roofline"]["bucket_parts"]["parts"] == 2
     # one MSM per step whatever the world: value = n * steps / time
     assert d2["value"] == pytest.approx(65536 * 2 / (d2["ms_per_step"] * 2e-3), rel=1e-6)
+    assert d2["bit_exact_vs_unsplit"] is True  # the fold against an unsplit commit, every rank
+
+
+@pytest.mark.gpu
+def test_msm_split_points_over_ranks_line():
+    """`--msm-split points` on 2 gloo ranks (round-5 advisor: each rank commits ITS span of the
+    scalars against its SRS slice, not the whole vector), checked against an unsplit commit."""
+    d = run_bench("--gpus", "2", "--mode", "msm", "--shard-msm", "--msm-split", "points",
+                  "--dist-backend", "gloo", "--log-n", "16", "--steps", "2", "--warmup", "1",
+                  timeout=300)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "msm-split x2 (points)"
+    assert "SRS slice" in d["config"]["workload"] and d["bit_exact_vs_unsplit"] is True
 
 
 class _FakeSplitParams:
@@ -312,10 +324,12 @@ def _msm_shard_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_msm_shard_point_gloo_world2():
+@pytest.mark.parametrize("world", [2, 4])
+def test_msm_shard_point_gloo(world):
     """The msm_shard field of the default multi-rank line (the north star's MSM curve): ONE
-    MSM per step split over 2 gloo ranks by bucket range, shares all-gathered and folded, the
-    fold checked against the unsplit commit on every rank (CPU: the split restated by pyref)."""
+    MSM per step split over 2 / 4 gloo ranks by bucket range, shares all-gathered and folded,
+    the fold checked against the unsplit commit on every rank (CPU: the split restated by
+    pyref)."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as sk:
@@ -323,13 +337,13 @@ def test_msm_shard_point_gloo_world2():
         port = sk.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_msm_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_msm_shard_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
-    out = dict(q.get(timeout=5) for _ in range(2))
-    assert out == {0: True, 1: True}
+    out = dict(q.get(timeout=5) for _ in range(world))
+    assert out == {r: True for r in range(world)}
     for p in procs:
         assert p.exitcode == 0
 

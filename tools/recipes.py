@@ -100,6 +100,7 @@ def r_refresh(o, a):
     tool(o, "pmc_summary.txt", "tools/pmc_summary.py", str(o / "pmc"), str(o / "pmc_traffic.json"))
     for k in (20, 16):
         trace(o, f"bd{k}", f"--log-n {k} --lanes 1 --steps 2 --warmup 1 --no-cpu-baseline --no-extras")
+        tool(o, f"bd{k}.txt", "tools/trace_breakdown.py", str(o / f"bd{k}" / "run_kernel_trace.csv"))
 
 
 def r_configs(o, a):
