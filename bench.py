@@ -663,7 +663,7 @@ def load_pmc_traffic(kernel_substr: str, key: str = "hbm_bytes_per_launch",
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, made by tools/gpu_pmc.sh + tools/pmc_summary.py from the
     default bench command). key "hbm_bytes_last_launch" = the run's last dispatch. A summary
-    with a "units" field (tools/gpu_configs.sh: the transforms or MSMs its run performed)
+    with a "units" field (tools/recipes.py configs: the transforms or MSMs its run performed)
     gives bytes per unit instead: all launches of the kernel / units."""
     f = ROOT / "profiles" / fname
     if not f.exists():

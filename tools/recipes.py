@@ -111,6 +111,12 @@ def r_configs(o, a):
         trace(o, f"prof_{m}", f"--mode {m} --log-n 20 --steps 10 --warmup 2 --no-cpu-baseline", 300)
         pmc(o, f"pmc_{m}", "FETCH_SIZE;WRITE_SIZE",
             f"--mode {m} --log-n 20 --steps 10 --warmup 2 --no-cpu-baseline", 120)
+        out = o / f"pmc_traffic_{m}20.json"
+        tool(o, f"pmc_{m}_summary.txt", "tools/pmc_summary.py", str(o / f"pmc_{m}"), str(out))
+        # bytes per unit = all launches / the transforms (dft + idft per step) or MSMs of the run
+        d = json.loads(out.read_text())
+        d["units"] = (10 + 2) * (2 if m == "ntt" else 1)
+        out.write_text(json.dumps(d, indent=1, sort_keys=True))
     for m, k in (("ntt", 20), ("msm", 20), ("ntt", 23), ("msm", 16)):
         bench(o, "lines", f"--mode {m} --log-n {k} --steps 10 --warmup 2", 300, append=True)
     bench(o, "lines", "--mode msm --log-n 20 --steps 20 --warmup 3 --no-cpu-baseline --bucket-parts 8",
