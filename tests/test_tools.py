@@ -12,7 +12,7 @@ def test_recipes_list():
                        text=True, timeout=60)
     assert p.returncode == 0, p.stderr
     names = [ln.split()[0] for ln in p.stdout.splitlines() if ln.strip()]
-    assert names == sorted(["ab", "check", "configs", "counters", "parts", "refresh", "sizes"])
+    assert names == sorted(["ab", "check", "configs", "counters", "parts", "refresh", "shardprobe", "sizes"])
 
 
 def test_recipe_ab_passes_its_options_to_ab_py(monkeypatch, tmp_path):

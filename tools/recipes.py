@@ -180,8 +180,22 @@ def r_check(o, a):
     bench(o, "bench_default", "--steps 20 --warmup 5", 600)
 
 
+def r_shardprobe(o, a):
+    """One rank's share of a bucket-split sharded 2^20 proof on ONE GPU (tools/shard_rank_probe.py:
+    the all-gather emulated, every kernel of the rank as on a node) at G = 2, 4, 8 (ranks 0 and
+    G - 1), beside an unsharded lane; a kernel trace of rank 0 of 8 for the per-kernel breakdown."""
+    for g in (2, 4, 8):
+        for r in sorted({0, g - 1}):
+            run([PY, "tools/shard_rank_probe.py", "--world", str(g), "--rank", str(r), "--proofs", "4"],
+                400, o / "probe.jsonl", append=True)
+    run(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", str(o / "trace8"),
+         "-o", "run", "--", "python3", "tools/shard_rank_probe.py", "--world", "8", "--rank", "0",
+         "--proofs", "2"], 400, o / "trace8.json")
+    tool(o, "trace8.txt", "tools/trace_breakdown.py", str(o / "trace8" / "run_kernel_trace.csv"))
+
+
 RECIPES = {"refresh": r_refresh, "configs": r_configs, "sizes": r_sizes, "parts": r_parts,
-           "counters": r_counters, "ab": r_ab, "check": r_check}
+           "counters": r_counters, "ab": r_ab, "check": r_check, "shardprobe": r_shardprobe}
 
 
 def main() -> int:
