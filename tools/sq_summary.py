@@ -1,4 +1,4 @@
-"""Per-kernel averages of the SQ counters collected by tools/gpu_sq.sh."""
+"""Per-kernel averages of the SQ counters of a rocprofv3 --pmc run (tools/recipes.py counters)."""
 import collections
 import csv
 import sys
