@@ -18,6 +18,11 @@ value = constraints/s = n * proofs / max-over-ranks time.
     split over the ranks by bucket range (plk_prover_shard_buckets, round 6) or, where the
     SRS does not allow that split, by SRS slice (plk_prover_shard): one RCCL all-gather of
     partial points per commit group, host fold — strong scaling of proof latency.
+After the timed region the prove line also carries (unless --no-extras) `msm_shard`: one 2^k
+MSM split over ALL ranks by bucket range (RCCL all-gather + host fold, checked against the
+unsplit commit; at world 1 the lone MSM against the oracle) — the north star's MSM scaling
+curve, one point per run — and `n_2_16`: the metric's second size, a short 2^16 prove run.
+Every line carries `build_id` (plk_build_info, checked against this tree before anything runs).
 `--gpus N` without a launcher starts N ranks itself (torch.distributed.run, 127.0.0.1).
 Other modes: hotpath (only the NTT/MSM calls of one proof), ntt / msm (BASELINE configs[1] /
 [2], checked bit-exact against the oracle after the timed loop).
