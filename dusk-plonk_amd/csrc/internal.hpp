@@ -1,7 +1,5 @@
 // internal.hpp — shared runtime objects behind the C ABI (include/plk.h).
 #pragma once
-#include <chrono>
-#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <map>
@@ -183,17 +181,6 @@ struct PinnedBuf {
 // Host wait for all work queued on `s`, blocking in the driver instead of spinning: the
 // prover's host thread waits at every commitment, and a spinning wait steals the core a
 // concurrent composer synthesis (or any other host work) runs on. One event per thread.
-// PLK_SPIN_US (read once): poll the event for up to that many microseconds before blocking —
-// a blocked thread's wake-up adds tens of µs to every wait, which small proofs (a few ms,
-// ~5 waits each) feel; large proofs' waits outlast any spin and block as before.
-inline uint32_t spin_us() {
-  static const uint32_t v = [] {
-    const char* e = getenv("PLK_SPIN_US");
-    const long x = e ? atol(e) : 0;
-    return (uint32_t)(x > 0 ? x : 0);
-  }();
-  return v;
-}
 inline hipError_t stream_wait(hipStream_t s) {
   thread_local hipEvent_t ev = nullptr;
   if (!ev) {
@@ -202,14 +189,6 @@ inline hipError_t stream_wait(hipStream_t s) {
   }
   const hipError_t e = hipEventRecord(ev, s);
   if (e != hipSuccess) return e;
-  if (const uint32_t us = spin_us()) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-      const hipError_t q = hipEventQuery(ev);
-      if (q != hipErrorNotReady) return q;
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us)) break;
-    }
-  }
   return hipEventSynchronize(ev);
 }
 
