@@ -474,10 +474,112 @@ constexpr RxColOrder<sizeof...(KINDS)> rx_col_order() {
   return o;
 }
 
+}  // namespace plk
+#include "rx_asm_gen.hpp"
+namespace plk {
+// The ASM form of a product group (round 6; the lane form of k_accumulate): each column of an
+// Fp group as ONE inline-asm statement holding its interleaved v_mad_u64_u32 in
+// rx_col_order's order, so that no empty pin sits between the mads and the hazard recognizer
+// pads only where the column's closing instructions read the statement's outputs: 420-440 -> 67-77
+// s_nop and 4 855-4 873 -> 4 501-4 509 instructions in k_accumulate's loop block (same 3 056
+// v_mad_u64_u32; hipcc -S of msm_acc.hip, both lane-form instantiations). The statement's text is built here
+// at compile time; its operand list (the accumulator slots, the first factors, the variable
+// second factors in VGPRs and the limbs of p in SGPRs) comes from rx_asm_gen.hpp
+// (tools/gen_rx_asm.py). Measured (profiles/r06_asm_columns_ab.jsonl, three interleaved runs):
+// solo additions/s in the 2^20 proof 6.97 -> 7.02e9 and in the 2^16 proof 5.28 -> 5.55e9,
+// proofs 32.55 -> 32.80 M (2^20) and 26.28 -> 26.91 M (2^16); the same form in the run sums'
+// full additions (triples, at 1 wave per SIMD) measured no better and is not used there.
+struct RxAsmText {
+  char s[8192];
+  int len;
+  constexpr const char* data() const { return s; }
+  constexpr unsigned long size() const { return (unsigned long)len; }
+};
+constexpr void rx_asm_put(RxAsmText& t, const char* x) {
+  for (int i = 0; x[i]; ++i) t.s[t.len++] = x[i];
+}
+constexpr void rx_asm_num(RxAsmText& t, int v) {
+  char b[8] = {};
+  int n = 0;
+  do {
+    b[n++] = (char)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  while (n) t.s[t.len++] = b[--n];
+}
+// Whether mad e of column K multiplies by a constant (a limb of p: a Montgomery reduction
+// term), in rx_group_column's term order; `first`: its accumulator starts there.
+struct RxAsmTerm {
+  int slot, red, first;
+};
+template <class C, int K, int... KINDS>
+struct RxAsmPlan {
+  static constexpr int NP = sizeof...(KINDS);
+  RxAsmTerm t[3 * 26 * 4] = {};
+  int n = 0, nv = 0, ns = 0;
+  int used[3 * NP] = {};  // the slot takes a term in this column
+  constexpr RxAsmPlan() {
+    constexpr int L = RxShape<C>::L;
+    constexpr int kind[NP] = {KINDS...};
+    constexpr RxPlan<C, 1> P1{};
+    constexpr RxPlan<C, 2> P2{};
+    constexpr RxColOrder<NP> ord = rx_col_order<C, K, KINDS...>();
+    const int i0 = K < L ? 0 : K - L + 1, i1 = K < L ? K : L - 1;
+    const int n1 = i1 - i0 + 1;
+    const int ncross = (K + 1) / 2 - i0 > 0 ? (K + 1) / 2 - i0 : 0;
+    const int nsq = ncross + ((K & 1) == 0 ? 1 : 0);
+    int pos[3 * NP] = {};
+    n = ord.n;
+    for (int e = 0; e < n; ++e) {
+      const int q = ord.acc[e], p = q / 3, which = q % 3;
+      const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+      const int nprod = which != 0 ? 0 : kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? nsq
+                                       : (split ? n1 : 2 * n1);
+      const int tt = pos[q]++;
+      t[e].slot = q;
+      t[e].red = which == 1 || (which == 0 && tt >= nprod);
+      t[e].first = tt == 0 && (which != 0 || K == 0);
+      if (t[e].red) ++ns; else ++nv;
+      used[q] = 1;
+    }
+  }
+};
+// mad e: v_mad_u64_u32 %slot, vcc, %(S + e), %(its second factor), %slot — or 0 as the addend
+// when the slot starts there (s2 / s3 of a split column, the first column's accumulators).
+// Operands: S slots, N first factors, NV variable second factors, NS constant ones.
+template <class C, int K, int... KINDS>
+constexpr RxAsmText rx_asm_text() {
+  constexpr RxAsmPlan<C, K, KINDS...> P{};
+  const int S = 3 * P.NP, N = P.n;
+  RxAsmText t{};
+  int jv = 0, js = 0;
+  for (int e = 0; e < N; ++e) {
+    const RxAsmTerm& m = P.t[e];
+    rx_asm_put(t, "v_mad_u64_u32 %");
+    rx_asm_num(t, m.slot);
+    rx_asm_put(t, ", vcc, %");
+    rx_asm_num(t, S + e);
+    rx_asm_put(t, ", %");
+    rx_asm_num(t, m.red ? S + N + P.nv + js++ : S + N + jv++);
+    if (m.first) {
+      rx_asm_put(t, ", 0\n");
+    } else {
+      rx_asm_put(t, ", %");
+      rx_asm_num(t, m.slot);
+      rx_asm_put(t, "\n");
+    }
+  }
+  return t;
+}
+template <class C, int K, int... KINDS>
+struct RxAsmTextK {
+  static constexpr RxAsmText text = rx_asm_text<C, K, KINDS...>();
+};
+
 // column K of every product of the group (K a template argument: every bound and branch
 // below is a compile-time constant). Each accumulator's terms are taken in a fixed order
 // (operand products first, then reduction terms); the interleaving is rx_col_order's.
-template <class C, int K, int... KINDS>
+template <class C, bool ASM, int K, int... KINDS>
 PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* const* a,
                             const Rx<C>* const* b, const Rx<C>* const* c, const Rx<C>* const* d,
                             Rx<C>* const* out) {
@@ -502,6 +604,45 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
     s2[p] = s3[p] = 0;
     pos[3 * p] = pos[3 * p + 1] = pos[3 * p + 2] = 0;
   }
+  constexpr bool kAsmCol = ASM && SPLIT_ON;
+  if constexpr (kAsmCol) {  // Fp: the column's mads as one asm statement (see RxAsmText)
+    constexpr RxAsmPlan<C, K, KINDS...> PLAN{};
+    uint32_t X[PLAN.n], Y[PLAN.nv > 0 ? PLAN.nv : 1], KP[PLAN.ns > 0 ? PLAN.ns : 1];
+    int jv = 0, js = 0;
+#pragma unroll
+    for (int e = 0; e < ord.n; ++e) {
+      const int q = ord.acc[e], p = q / 3, which = q % 3;
+      const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+      const int t = pos[q]++;
+      const int nprod = which != 0 ? 0 : kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? nsq
+                                       : (split ? n1 : 2 * n1);
+      if (which == 2) {
+        X[e] = c[p]->v[i0 + t]; Y[jv++] = d[p]->v[K - i0 - t];
+      } else if (which == 1 || t >= nprod) {
+        const int i = rfirst + (which == 1 ? t : t - nprod);
+        X[e] = g.m[p][i]; KP[js++] = KC.p[K - i];
+      } else if (kind[p] == kRxSqr) {
+        if (t < ncross) { X[e] = a[p]->v[i0 + t]; Y[jv++] = g.a2[p][K - i0 - t]; }
+        else { X[e] = a[p]->v[K / 2]; Y[jv++] = a[p]->v[K / 2]; }
+      } else if (t < n1) {
+        X[e] = a[p]->v[i0 + t]; Y[jv++] = b[p]->v[K - i0 - t];
+      } else {
+        X[e] = c[p]->v[i0 + t - n1]; Y[jv++] = d[p]->v[K - i0 - t + n1];
+      }
+    }
+    // s2 / s3 are output-only operands (rx_asm_gen.hpp); the carried accumulators go in
+    uint64_t slot[3 * NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) slot[3 * p] = g.acc[p];
+    RxAsmRun<PLAN.nv, PLAN.ns, 3 * NP>::template run<RxAsmTextK<C, K, KINDS...>>(slot, X, Y, KP);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {  // a slot the column does not use stays 0 (rx_column_close)
+      g.acc[p] = slot[3 * p];
+      s2[p] = PLAN.used[3 * p + 1] ? slot[3 * p + 1] : 0;
+      s3[p] = PLAN.used[3 * p + 2] ? slot[3 * p + 2] : 0;
+    }
+  }
+  if constexpr (!kAsmCol) {
 #pragma unroll
   for (int e = 0; e < ord.n; ++e) {
     const int q = ord.acc[e], p = q / 3, which = q % 3;
@@ -526,6 +667,7 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
     }
     rx_pin(dst);
   }
+  }
   (void)rlast;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
@@ -534,15 +676,16 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
   }
 }
 
-template <class C, int... KINDS, int... KS>
+template <class C, bool ASM, int... KINDS, int... KS>
 PLK_RX void rx_group_columns(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* const* a,
                              const Rx<C>* const* b, const Rx<C>* const* c,
                              const Rx<C>* const* d, Rx<C>* const* out,
                              std::integer_sequence<int, KS...>) {
-  (rx_group_column<C, KS, KINDS...>(g, a, b, c, d, out), ...);
+  (rx_group_column<C, ASM, KS, KINDS...>(g, a, b, c, d, out), ...);
 }
 
-template <class C, int... KINDS>
+// ASM: the columns as single asm statements (Fp only; see RxAsmText)
+template <class C, bool ASM, int... KINDS>
 PLK_RX void rx_prod_group(const Rx<C>* const* a, const Rx<C>* const* b, const Rx<C>* const* c,
                           const Rx<C>* const* d, Rx<C>* const* out) {
   constexpr int L = RxShape<C>::L;
@@ -557,25 +700,26 @@ PLK_RX void rx_prod_group(const Rx<C>* const* a, const Rx<C>* const* b, const Rx
       for (int i = 0; i < L; ++i) g.a2[p][i] = a[p]->v[i] << 1;
     }
   }
-  rx_group_columns<C, KINDS...>(g, a, b, c, d, out, std::make_integer_sequence<int, 2 * L - 1>{});
+  rx_group_columns<C, ASM, KINDS...>(g, a, b, c, d, out,
+                                     std::make_integer_sequence<int, 2 * L - 1>{});
 #pragma unroll
   for (int p = 0; p < NP; ++p) out[p]->v[L - 1] = (uint32_t)g.acc[p];
 }
 
 // the pair / triple forms used by the group law
-template <class C>
+template <class C, bool ASM = false>
 PLK_RX void rx_mul2(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& a1, const Rx<C>& b1,
                     Rx<C>& o0, Rx<C>& o1) {
   const Rx<C>* a[2] = {&a0, &a1};
   const Rx<C>* b[2] = {&b0, &b1};
   Rx<C>* o[2] = {&o0, &o1};
-  rx_prod_group<C, kRxMul, kRxMul>(a, b, a, b, o);
+  rx_prod_group<C, ASM, kRxMul, kRxMul>(a, b, a, b, o);
 }
-template <class C>
+template <class C, bool ASM = false>
 PLK_RX void rx_sqr2(const Rx<C>& a0, const Rx<C>& a1, Rx<C>& o0, Rx<C>& o1) {
   const Rx<C>* a[2] = {&a0, &a1};
   Rx<C>* o[2] = {&o0, &o1};
-  rx_prod_group<C, kRxSqr, kRxSqr>(a, a, a, a, o);
+  rx_prod_group<C, ASM, kRxSqr, kRxSqr>(a, a, a, a, o);
 }
 template <class C>
 PLK_RX void rx_mul3(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& a1, const Rx<C>& b1,
@@ -583,11 +727,11 @@ PLK_RX void rx_mul3(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& a1, const Rx<
   const Rx<C>* a[3] = {&a0, &a1, &a2};
   const Rx<C>* b[3] = {&b0, &b1, &b2};
   Rx<C>* o[3] = {&o0, &o1, &o2};
-  rx_prod_group<C, kRxMul, kRxMul, kRxMul>(a, b, a, b, o);
+  rx_prod_group<C, false, kRxMul, kRxMul, kRxMul>(a, b, a, b, o);
 }
 // (a0 b0 + c0 d0, a1 b1, a2 b2): the fused Y3 beside ZZ3 and ZZZ3 (its 2 product sets
 // against their one each: the three accumulators alternate)
-template <class C>
+template <class C, bool ASM = false>
 PLK_RX void rx_mul_add_mul2(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& c0, const Rx<C>& d0,
                             const Rx<C>& a1, const Rx<C>& b1, const Rx<C>& a2, const Rx<C>& b2,
                             Rx<C>& o0, Rx<C>& o1, Rx<C>& o2) {
@@ -596,7 +740,7 @@ PLK_RX void rx_mul_add_mul2(const Rx<C>& a0, const Rx<C>& b0, const Rx<C>& c0, c
   const Rx<C>* c[3] = {&c0, &c0, &c0};
   const Rx<C>* d[3] = {&d0, &d0, &d0};
   Rx<C>* o[3] = {&o0, &o1, &o2};
-  rx_prod_group<C, kRxMulAdd, kRxMul, kRxMul>(a, b, c, d, o);
+  rx_prod_group<C, ASM, kRxMulAdd, kRxMul, kRxMul>(a, b, c, d, o);
 }
 
 // a + b mod 2p-range: [0, 2p) + [0, 2p) -> [0, 2p)

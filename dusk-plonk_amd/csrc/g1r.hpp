@@ -140,18 +140,21 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
 // it is the faster form where the chip is otherwise idle (lone 2^20 MSM 2.84-2.85 against
 // 2.92 ms). Measured and dropped in round 5: (PPP, Q, ZZ3) + (Y3, ZZZ3) (round 4's libplk-g2)
 // and (PPP, ZZ3) + (Q, ZZZ3) + Y3 alone, both spilling at 3 waves.
-template <bool GROUPED>
+// ASM (round 6, k_accumulate's lane form): the groups' columns as single asm statements
+// (ffr.hpp RxAsmText): ~4 505 instructions and ~72 s_nop per loop iteration instead of ~4 865 /
+// ~430.
+template <bool GROUPED, bool ASM = false>
 __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, const RFp& y2) {
   if constexpr (GROUPED) {
     RFp U2, S2, PP, RR, PPP, Q;
-    rx_mul2(x2, p.ZZ, y2, p.ZZZ, U2, S2);
+    rx_mul2<FpCfg, ASM>(x2, p.ZZ, y2, p.ZZZ, U2, S2);
     const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
     const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
-    rx_sqr2(P, R, PP, RR);
+    rx_sqr2<FpCfg, ASM>(P, R, PP, RR);
     G1R r;
-    rx_mul2(P, PP, p.X, PP, PPP, Q);
+    rx_mul2<FpCfg, ASM>(P, PP, p.X, PP, PPP, Q);
     r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
-    rx_mul_add_mul2(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP,
+    rx_mul_add_mul2<FpCfg, ASM>(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP,
                     p.ZZ, PP, p.ZZZ, PPP, r.Y, r.ZZ, r.ZZZ);
     return r;
   } else {

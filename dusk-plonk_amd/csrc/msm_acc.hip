@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(kAccThreads)
     if (HAS_INF && cur_inf) continue;
     if (cur & 0x80000000u) y = rx_neg_lazy(y);
     const bool was_inf = g1r_is_inf(acc);
-    G1R r = g1r_madd_lazy_sl<!LONE>(acc, x, y);
+    G1R r = g1r_madd_lazy_sl<!LONE, !LONE>(acc, x, y);
     if (rx_is_zero(r.ZZ)) {  // rare: reload the point rather than keep it live
       RFp xr, yr;
       ld_g1r_aff(&table[cur & 0x7fffffffu], xr, yr);

@@ -28,3 +28,17 @@ def test_recipe_ab_passes_its_options_to_ab_py(monkeypatch, tmp_path):
     for flag, val in (("--lib", "a=libplk.so"), ("--venv", "q=PLK_TAIL_QUAD=0"),
                       ("--args", "--log-n 12"), ("--env", "PLK_LIB_ANY_SRC=1"), ("--reps", "3")):
         assert cmd[cmd.index(flag) + 1] == val
+
+
+def test_rx_asm_gen_header_is_current(tmp_path, monkeypatch):
+    """dusk-plonk_amd/csrc/rx_asm_gen.hpp is what tools/gen_rx_asm.py writes (the asm-column
+    operand lists must cover every column shape ffr.hpp's rx_col_order produces)."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    try:
+        import gen_rx_asm
+    finally:
+        sys.path.pop(0)
+    out = tmp_path / "rx_asm_gen.hpp"
+    monkeypatch.setattr(gen_rx_asm, "OUT", out)
+    gen_rx_asm.main()
+    assert out.read_text() == (ROOT / "dusk-plonk_amd" / "csrc" / "rx_asm_gen.hpp").read_text()
