@@ -142,10 +142,25 @@ __device__ __forceinline__ G1R g1r_add(const G1R& p, const G1R& q) {
 // and (PPP, ZZ3) + (Q, ZZZ3) + Y3 alone, both spilling at 3 waves.
 // ASM (round 6, k_accumulate's lane form): the groups' columns as single asm statements
 // (ffr.hpp RxAsmText): ~4 505 instructions and ~72 s_nop per loop iteration instead of ~4 865 /
-// ~430.
-template <bool GROUPED, bool ASM = false>
+// ~430. PAIRS (with ASM): Y3 as a plain product and (ZZ3, ZZZ3) as a pair instead of the
+// triple group: 168 VGPRs, so it fits 3 waves per SIMD without spilling (k_accumulate's lone
+// form since round 6; the plain chains below are the formula as one product at a time, the
+// lone form before).
+template <bool GROUPED, bool ASM = false, bool PAIRS = false>
 __device__ __forceinline__ G1R g1r_madd_lazy_sl(const G1R& p, const RFp& x2, const RFp& y2) {
-  if constexpr (GROUPED) {
+  if constexpr (GROUPED && PAIRS) {
+    RFp U2, S2, PP, RR, PPP, Q;
+    rx_mul2<FpCfg, ASM>(x2, p.ZZ, y2, p.ZZZ, U2, S2);
+    const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);
+    const RFp R = rx_sub_u<FpCfg, 6>(S2, p.Y);
+    rx_sqr2<FpCfg, ASM>(P, R, PP, RR);
+    G1R r;
+    rx_mul2<FpCfg, ASM>(P, PP, p.X, PP, PPP, Q);
+    r.X = rx_sub2_n<FpCfg, 6>(RR, PPP, Q);
+    r.Y = rx_mul_add(R, rx_sub_u<FpCfg, 10>(Q, r.X), rx_sub_u<FpCfg, 5>(rx_zero<FpCfg>(), p.Y), PPP);
+    rx_mul2<FpCfg, ASM>(p.ZZ, PP, p.ZZZ, PPP, r.ZZ, r.ZZZ);
+    return r;
+  } else if constexpr (GROUPED) {
     RFp U2, S2, PP, RR, PPP, Q;
     rx_mul2<FpCfg, ASM>(x2, p.ZZ, y2, p.ZZZ, U2, S2);
     const RFp P = rx_sub_u<FpCfg, 10>(U2, p.X);

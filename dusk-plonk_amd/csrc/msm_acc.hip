@@ -57,9 +57,14 @@ __device__ __forceinline__ void unstage_point(const uint4 (*stage)[64], uint32_t
 }
 
 // LONE: the form for a chip the MSM has to itself (lone commits, plk_prove's default
-// prover): plain product chains at 3 waves per SIMD; otherwise (prover lanes, several proofs
-// sharing the chip) the interleaved product groups at 2 (g1r.hpp g1r_madd_lazy_sl; round 5
-// A/B, profiles/r05_acc_dma_ab.jsonl)
+// prover): at 3 waves per SIMD, product PAIRS (168 VGPRs, no spill); otherwise (prover lanes,
+// several proofs sharing the chip) the interleaved groups with the (Y3, ZZ3, ZZZ3) triple at 2
+// (g1r.hpp g1r_madd_lazy_sl; round 5 A/B, profiles/r05_acc_dma_ab.jsonl). Both with the group
+// columns as single asm statements (round 6). The lone form was plain product chains until
+// then (4 648 instructions and 311 64-bit merge adds per loop iteration against 4 500 / 114 for
+// the asm pairs; lone 2^20 MSM 2.81 -> 2.80 ms, 7.42 -> 7.51e9 solo additions/s over four
+// interleaved runs, profiles/r06_lone_asm_pairs_ab.jsonl; the lanes on this form at 3 waves
+// measured no better than the triple at 2).
 template <bool HAS_INF, bool LONE>
 __global__ void __launch_bounds__(kAccThreads)
     __attribute__((amdgpu_waves_per_eu(LONE ? 3 : 2, LONE ? 3 : 2)))
@@ -116,7 +121,7 @@ __global__ void __launch_bounds__(kAccThreads)
     if (HAS_INF && cur_inf) continue;
     if (cur & 0x80000000u) y = rx_neg_lazy(y);
     const bool was_inf = g1r_is_inf(acc);
-    G1R r = g1r_madd_lazy_sl<!LONE, !LONE>(acc, x, y);
+    G1R r = g1r_madd_lazy_sl<true, true, LONE>(acc, x, y);
     if (rx_is_zero(r.ZZ)) {  // rare: reload the point rather than keep it live
       RFp xr, yr;
       ld_g1r_aff(&table[cur & 0x7fffffffu], xr, yr);
