@@ -480,10 +480,11 @@ namespace plk {
 // The ASM form of a product group (round 6; the lane form of k_accumulate): each column of an
 // Fp group as ONE inline-asm statement holding its interleaved v_mad_u64_u32 in
 // rx_col_order's order, so that no empty pin sits between the mads and the hazard recognizer
-// pads only where the column's closing instructions read the statement's outputs: 420-440 -> 67-77
-// s_nop and 4 855-4 873 -> 4 501-4 509 instructions in k_accumulate's loop block (same 3 056
-// v_mad_u64_u32; hipcc -S of msm_acc.hip, both lane-form instantiations). The statement's text is built here
-// at compile time; its operand list (the accumulator slots, the first factors, the variable
+// pads only where the column's closing instructions read the statement's outputs: 420-440 ->
+// 67-77 s_nop and 4 855-4 873 -> 4 501-4 509 instructions in k_accumulate's loop block (same
+// 3 056 v_mad_u64_u32; hipcc -S of msm_acc.hip, both lane-form instantiations). The statement's
+// text is built here at compile time; its operand list (the accumulator slots, the first
+// factors, the variable
 // second factors in VGPRs and the limbs of p in SGPRs) comes from rx_asm_gen.hpp
 // (tools/gen_rx_asm.py). Measured (profiles/r06_asm_columns_ab.jsonl, three interleaved runs):
 // solo additions/s in the 2^20 proof 6.97 -> 7.02e9 and in the 2^16 proof 5.28 -> 5.55e9,
