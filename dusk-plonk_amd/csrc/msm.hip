@@ -676,8 +676,17 @@ inline size_t run_lanes() {
   }();
   return v;
 }
+// a batch's rb: kRunBits, or PLK_RUN_BITS_BATCH from the environment (sweeps; 1 .. 8)
+inline uint32_t batch_run_bits() {
+  static const uint32_t v = [] {
+    const char* e = getenv("PLK_RUN_BITS_BATCH");
+    const int x = e ? atoi(e) : 0;
+    return x >= 1 && x <= 8 ? (uint32_t)x : kRunBits;
+  }();
+  return v;
+}
 inline uint32_t run_bits(uint32_t B, uint32_t slots) {
-  if (slots > 1) return kRunBits;
+  if (slots > 1) return std::min<uint32_t>(batch_run_bits(), 31 - __builtin_clz(B));
   uint32_t rb = kRunBits;
   while (rb > kRunBitsMin && (size_t)(B >> rb) < run_lanes()) --rb;
   return rb;
@@ -1351,7 +1360,8 @@ int ws_reserve(plk_srs* s, MsmWorkspace& w, size_t len, uint32_t slots, hipStrea
   const size_t NC = B >> kFineBits;
   // runs over all slots of a batch (run_bits: a batch runs B >> kRunBits per slot, a lone
   // MSM fewer than 2 kRunLanes unless rb = kRunBits)
-  const size_t max_runs = std::max<size_t>(slots * (B >> kRunBits), B >> kRunBitsMin);
+  const size_t max_runs =
+      std::max<size_t>(slots * (B >> std::min(kRunBits, batch_run_bits())), B >> kRunBitsMin);
   if (wide && NC > kCoarseMax) return PLK_E_ARG;
   const size_t entries = (size_t)s->windows * len;
   // small shapes (k_sort_one's) may run tasks of kChunkSmall points (msm_run_batch)
