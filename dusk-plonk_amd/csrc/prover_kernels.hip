@@ -207,34 +207,58 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_tops(Fr* __restrict__ tot
 }
 
 // Small scans (n <= kScanSingleMax) in ONE dispatch: a workgroup of 1 024 threads, thread t
-// owning the per = ceil(n / 1024) consecutive logical elements from t * per (reduce, block
-// scan of the thread totals in LDS, apply). Small proofs are bound by the rate at which the
-// command processor takes dispatches (~140 k/s with 16 lanes), and the 3-phase
-// form is 3 of them per scan.
+// owning the per = ceil(n / 1024) consecutive logical elements from t * per (reduce, scan of
+// the thread totals, apply). Small proofs are bound by the rate at which the command
+// processor takes dispatches (~140 k/s with 16 lanes), and the 3-phase form is 3
+// of them per scan.
 // (round 5: the 3-phase form from n > 4096 instead measured no faster at 2^13-2^15 proofs,
 // profiles/r05_scan_buckets_lds_ab.jsonl)
+// The thread totals are scanned inside each wave by shuffles (6 levels, no barrier), the 16
+// wave totals by wave 0 the same way, with two barriers in all (round 6; the LDS
+// Hillis-Steele scan it replaces took 10 levels over all 16 waves and 20 barriers).
 constexpr uint32_t kScanSingleThreads = 1024, kScanSingleMax = 32 * kScanSingleThreads;
+constexpr uint32_t kScanSingleWaves = kScanSingleThreads / 64;
+__device__ __forceinline__ Fr shfl_up_fr(const Fr& v, uint32_t h) {
+  Fr o;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o.v[k] = (uint32_t)__shfl_up((int)v.v[k], h, 64);
+  return o;
+}
+// inclusive scan over the 64 lanes of a wave (lane order = operand order)
+template <bool MUL>
+__device__ __forceinline__ Fr wave_scan_incl(Fr v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t h = 1; h < 64; h <<= 1) {
+    const Fr o = shfl_up_fr(v, h);
+    if (lane >= h) v = op<MUL>(o, v);
+  }
+  return v;
+}
 // tot[nb] = the grand total, as the 3-phase form leaves it (the grand product's caller reads it)
 template <bool MUL, bool SUFFIX, bool EXCL>
 __global__ void __launch_bounds__(kScanSingleThreads) k_scan_single(const Fr* __restrict__ in,
                                                                     uint64_t n, Fr* __restrict__ out,
                                                                     Fr* __restrict__ tot, uint32_t nb) {
-  __shared__ Fr sh[kScanSingleThreads];
-  const uint32_t tid = threadIdx.x;
+  __shared__ Fr sh[kScanSingleWaves];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t per = (uint32_t)((n + kScanSingleThreads - 1) / kScanSingleThreads);
   const uint64_t base = (uint64_t)tid * per;
   Fr acc = ident<MUL>();
   for (uint32_t k = 0; k < per && base + k < n; ++k) acc = op<MUL>(acc, ldf(&in[phys<SUFFIX>(base + k, n)]));
-  sh[tid] = acc;
+  const Fr incl = wave_scan_incl<MUL>(acc, lane);  // this wave's threads 0 .. lane
+  if (lane == 63) sh[wave] = incl;
   __syncthreads();
-  for (uint32_t off = 1; off < kScanSingleThreads; off <<= 1) {
-    Fr v = tid >= off ? sh[tid - off] : ident<MUL>();
-    __syncthreads();
-    sh[tid] = op<MUL>(sh[tid], v);
-    __syncthreads();
+  if (wave == 0) {  // exclusive prefixes of the wave totals; sh[last] -> the grand total
+    const Fr w = lane < kScanSingleWaves ? sh[lane] : ident<MUL>();
+    const Fr wi = wave_scan_incl<MUL>(w, lane);
+    const Fr we = shfl_up_fr(wi, 1);
+    if (lane < kScanSingleWaves) sh[lane] = lane ? we : ident<MUL>();
+    if (lane == kScanSingleWaves - 1) stf(&tot[nb], wi);
   }
-  Fr run = tid ? sh[tid - 1] : ident<MUL>();
-  if (tid == kScanSingleThreads - 1) stf(&tot[nb], sh[tid]);
+  __syncthreads();
+  const Fr excl_in_wave = shfl_up_fr(incl, 1);
+  Fr run = lane ? (wave ? op<MUL>(sh[wave], excl_in_wave) : excl_in_wave)
+                : (wave ? sh[wave] : ident<MUL>());
   for (uint32_t k = 0; k < per && base + k < n; ++k) {
     const uint64_t p = phys<SUFFIX>(base + k, n);
     const Fr v = ldf(&in[p]);
