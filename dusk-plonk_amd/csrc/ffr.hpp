@@ -490,6 +490,8 @@ namespace plk {
 // solo additions/s in the 2^20 proof 6.97 -> 7.02e9 and in the 2^16 proof 5.28 -> 5.55e9,
 // proofs 32.55 -> 32.80 M (2^20) and 26.28 -> 26.91 M (2^16); the same form in the run sums'
 // full additions (triples, at 1 wave per SIMD) measured no better and is not used there.
+// Fr (no split columns, one accumulator per product: RxAsmRun1) takes the same form in the
+// NTT pass's pairs (ntt.hip twmul2).
 struct RxAsmText {
   char s[8192];
   int len;
@@ -516,6 +518,9 @@ struct RxAsmTerm {
 template <class C, int K, int... KINDS>
 struct RxAsmPlan {
   static constexpr int NP = sizeof...(KINDS);
+  // split shapes (Fp): 3 slots per product (acc, s2, s3); otherwise (Fr) one, the acc
+  static constexpr bool SPL = RxSplitOn<C>::value;
+  static constexpr int S = SPL ? 3 * NP : NP;
   RxAsmTerm t[3 * 26 * 4] = {};
   int n = 0, nv = 0, ns = 0;
   int used[3 * NP] = {};  // the slot takes a term in this column
@@ -533,11 +538,11 @@ struct RxAsmPlan {
     n = ord.n;
     for (int e = 0; e < n; ++e) {
       const int q = ord.acc[e], p = q / 3, which = q % 3;
-      const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+      const bool split = SPL && (kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K]);
       const int nprod = which != 0 ? 0 : kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? nsq
                                        : (split ? n1 : 2 * n1);
       const int tt = pos[q]++;
-      t[e].slot = q;
+      t[e].slot = SPL ? q : p;
       t[e].red = which == 1 || (which == 0 && tt >= nprod);
       t[e].first = tt == 0 && (which != 0 || K == 0);
       if (t[e].red) ++ns; else ++nv;
@@ -551,7 +556,7 @@ struct RxAsmPlan {
 template <class C, int K, int... KINDS>
 constexpr RxAsmText rx_asm_text() {
   constexpr RxAsmPlan<C, K, KINDS...> P{};
-  const int S = 3 * P.NP, N = P.n;
+  const int S = P.S, N = P.n;
   RxAsmText t{};
   int jv = 0, js = 0;
   for (int e = 0; e < N; ++e) {
@@ -605,15 +610,15 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
     s2[p] = s3[p] = 0;
     pos[3 * p] = pos[3 * p + 1] = pos[3 * p + 2] = 0;
   }
-  constexpr bool kAsmCol = ASM && SPLIT_ON;
-  if constexpr (kAsmCol) {  // Fp: the column's mads as one asm statement (see RxAsmText)
+  constexpr bool kAsmCol = ASM;
+  if constexpr (kAsmCol) {  // the column's mads as one asm statement (see RxAsmText)
     constexpr RxAsmPlan<C, K, KINDS...> PLAN{};
     uint32_t X[PLAN.n], Y[PLAN.nv > 0 ? PLAN.nv : 1], KP[PLAN.ns > 0 ? PLAN.ns : 1];
     int jv = 0, js = 0;
 #pragma unroll
     for (int e = 0; e < ord.n; ++e) {
       const int q = ord.acc[e], p = q / 3, which = q % 3;
-      const bool split = kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K];
+      const bool split = SPLIT_ON && (kind[p] == kRxMulAdd ? P2.split[K] : P1.split[K]);
       const int t = pos[q]++;
       const int nprod = which != 0 ? 0 : kind[p] == kRxMul ? n1 : kind[p] == kRxSqr ? nsq
                                        : (split ? n1 : 2 * n1);
@@ -631,16 +636,20 @@ PLK_RX void rx_group_column(RxGroupState<C, sizeof...(KINDS)>& g, const Rx<C>* c
         X[e] = c[p]->v[i0 + t - n1]; Y[jv++] = d[p]->v[K - i0 - t + n1];
       }
     }
-    // s2 / s3 are output-only operands (rx_asm_gen.hpp); the carried accumulators go in
-    uint64_t slot[3 * NP];
+    if constexpr (SPLIT_ON) {
+      // s2 / s3 are output-only operands (rx_asm_gen.hpp); the carried accumulators go in
+      uint64_t slot[3 * NP];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) slot[3 * p] = g.acc[p];
-    RxAsmRun<PLAN.nv, PLAN.ns, 3 * NP>::template run<RxAsmTextK<C, K, KINDS...>>(slot, X, Y, KP);
+      for (int p = 0; p < NP; ++p) slot[3 * p] = g.acc[p];
+      RxAsmRun<PLAN.nv, PLAN.ns, 3 * NP>::template run<RxAsmTextK<C, K, KINDS...>>(slot, X, Y, KP);
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {  // a slot the column does not use stays 0 (rx_column_close)
-      g.acc[p] = slot[3 * p];
-      s2[p] = PLAN.used[3 * p + 1] ? slot[3 * p + 1] : 0;
-      s3[p] = PLAN.used[3 * p + 2] ? slot[3 * p + 2] : 0;
+      for (int p = 0; p < NP; ++p) {  // a slot the column does not use stays 0 (rx_column_close)
+        g.acc[p] = slot[3 * p];
+        s2[p] = PLAN.used[3 * p + 1] ? slot[3 * p + 1] : 0;
+        s3[p] = PLAN.used[3 * p + 2] ? slot[3 * p + 2] : 0;
+      }
+    } else {  // one accumulator per product, carried in and out
+      RxAsmRun1<PLAN.nv, PLAN.ns, NP>::template run<RxAsmTextK<C, K, KINDS...>>(g.acc, X, Y, KP);
     }
   }
   if constexpr (!kAsmCol) {

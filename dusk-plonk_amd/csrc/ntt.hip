@@ -213,9 +213,13 @@ __device__ __forceinline__ RFr reduce_q(const RFr& a, const uint32_t* ztab) {
 __device__ __forceinline__ RFr twmul(const RFr& a, const uint32_t* twl, uint32_t TS, uint32_t idx) {
   return rx_mul(a, lds_ld(twl, TS, idx));
 }
+// Round 6: each column of the pair as one asm statement (ffr.hpp RxAsmText): 1 359 -> 1 294
+// instructions and 68 -> 1 s_nop in the main pass's loop block (123 -> 1 in the coset pass);
+// dft + idft 2^20 0.2844 -> 0.2812 ms, 2^23 1.972 -> 1.946 ms, proofs within noise (three
+// interleaved runs, profiles/r06_ntt_asm_pairs_ab.jsonl).
 __device__ __forceinline__ void twmul2(const RFr& a0, uint32_t i0, const RFr& a1, uint32_t i1,
                                        const uint32_t* twl, uint32_t TS, RFr& o0, RFr& o1) {
-  rx_mul2(a0, lds_ld(twl, TS, i0), a1, lds_ld(twl, TS, i1), o0, o1);
+  rx_mul2<FrCfg, true>(a0, lds_ld(twl, TS, i0), a1, lds_ld(twl, TS, i1), o0, o1);
 }
 
 // Two radix-2 DIF stages (halves 2h and h) on rows x0..x3 = j, j+h, j+2h, j+3h of one
