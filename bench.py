@@ -594,10 +594,11 @@ def host_info():
 
 
 def stored_clock(form_name: str):
-    """The stored DVFS reading of a k_accumulate form (profiles/r05_effective_clock.json: the
+    """The stored DVFS reading of a k_accumulate form (profiles/r06_effective_clock.json: the
     effective shader clock from GRBM_GUI_ACTIVE and the VALU activity per wave from the SQ
-    counters, one --pmc pass each, tools/gpu_r05_y.sh), or None."""
-    f = Path(__file__).resolve().parent / "profiles" / "r05_effective_clock.json"
+    counters on the round-6 final code, one --pmc pass each, tools/recipes.py counters), or
+    None."""
+    f = Path(__file__).resolve().parent / "profiles" / "r06_effective_clock.json"
     try:
         d = json.loads(f.read_text()).get(form_name)
     except (OSError, ValueError):
@@ -623,7 +624,7 @@ def valu_roofline(adds_per_s, form=ACC_LANE):
         dvfs = {"effective_clock_ghz": ghz,
                 "sq_valu_active_per_wave": clk["valu_per_wave"],
                 "waves_per_simd": clk["waves_per_simd"],
-                "source": "stored profiles/r05_effective_clock.json (" + clk["run"] + "): clock = "
+                "source": "stored profiles/r06_effective_clock.json (" + clk["run"] + "): clock = "
                           "GRBM_GUI_ACTIVE / 8 XCDs / dispatch time; SQ_ACTIVE_INST_VALU / "
                           "SQ_WAVE_CYCLES per wave (its product with the waves per SIMD is ~1.0 "
                           "here, but reads 1.3 for the NTT pass at 4 waves: the counter's active "

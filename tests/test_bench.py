@@ -92,7 +92,7 @@ def test_compiled_loop_mads():
 
 def test_valu_roofline_carries_stored_clock():
     """The VALU roofline of each k_accumulate form carries the stored DVFS reading
-    (profiles/r05_effective_clock.json: effective clock from GRBM_GUI_ACTIVE, the SQ VALU
+    (profiles/r06_effective_clock.json: effective clock from GRBM_GUI_ACTIVE, the SQ VALU
     activity per wave): the top-level frac is priced at the nominal 2.4 GHz."""
     sys.path.insert(0, str(ROOT))
     import bench
@@ -102,7 +102,7 @@ def test_valu_roofline_carries_stored_clock():
         assert d is not None, form
         assert 1.0 < d["effective_clock_ghz"] < 2.5
         assert 0.2 < d["sq_valu_active_per_wave"] < 1.0 and d["waves_per_simd"] in (2, 3)
-        assert "r05_effective_clock.json" in d["source"]
+        assert "r06_effective_clock.json" in d["source"]
 
 
 def test_gpus_flag_must_match_launcher():
